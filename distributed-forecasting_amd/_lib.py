@@ -1,0 +1,109 @@
+"""ctypes binding of ``libprophet_hip.so`` (the C ABI in include/prophet_hip.h).
+
+The library is built in-tree by ``build.py`` (hipcc --offload-arch=gfx950).
+There is deliberately NO fallback: if the shared library is missing or cannot
+be loaded, every engine entry point raises ``EngineUnavailable``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libprophet_hip.so")
+
+PF_GROWTH = {"linear": 0, "logistic": 1, "flat": 2}
+STATUS_NAMES = {0: "SUCCESS", 10: "ABSX", 20: "ABSF", 21: "RELF", 30: "ABSGRAD",
+                31: "RELGRAD", 40: "MAXIT", -1: "LSFAIL", -2: "BADINIT", 50: "CONSTANT"}
+PF_ST_CONSTANT = 50
+
+# Every symbol include/prophet_hip.h declares (checked by tests/test_abi.py).
+EXPORTED = ["pf_ctx_create", "pf_ctx_destroy", "pf_last_error", "pf_default_fit_opts",
+            "pf_num_changepoints", "pf_build_grid", "pf_prepare", "pf_objective_grad",
+            "pf_fit", "pf_predict"]
+
+
+class EngineUnavailable(RuntimeError):
+    pass
+
+
+vp = ctypes.c_void_p
+i32 = ctypes.c_int32
+
+
+class PfSeason(ctypes.Structure):
+    _fields_ = [("period", ctypes.c_double), ("order", i32), ("_pad", i32)]
+
+
+class PfGrid(ctypes.Structure):
+    _fields_ = [("T", i32), ("T_pad", i32), ("K", i32), ("S", i32),
+                ("t", vp), ("XT", vp), ("t_change", vp), ("seg", vp), ("cp_first", vp)]
+
+
+class PfProblem(ctypes.Structure):
+    _fields_ = [("n_series", i32), ("growth", i32), ("tau", ctypes.c_double),
+                ("grid", PfGrid),
+                ("sigmas", vp), ("s_a", vp), ("s_m", vp), ("y_scaled", vp), ("cap_scaled", vp),
+                ("fourier_orders", i32 * 3), ("season_mode", i32)]
+
+
+class PfFitOpts(ctypes.Structure):
+    _fields_ = [("init_alpha", ctypes.c_double), ("tol_obj", ctypes.c_double),
+                ("tol_rel_obj", ctypes.c_double), ("tol_grad", ctypes.c_double),
+                ("tol_rel_grad", ctypes.c_double), ("tol_param", ctypes.c_double),
+                ("max_iter", i32), ("history", i32), ("polish", i32), ("polish_max_iter", i32)]
+
+
+class PfPredictArgs(ctypes.Structure):
+    _fields_ = [("n_series", i32), ("growth", i32), ("n_samples", i32), ("_pad", i32),
+                ("fg", PfGrid),
+                ("s_a", vp), ("s_m", vp), ("theta", vp), ("y_scale", vp), ("cap_scaled", vp),
+                ("interval_width", ctypes.c_double), ("seed", ctypes.c_uint64),
+                ("yhat", vp), ("yhat_lower", vp), ("yhat_upper", vp),
+                ("trend", vp), ("trend_lower", vp), ("trend_upper", vp),
+                ("mult_terms", vp), ("add_terms", vp)]
+
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load the HIP engine library (raises EngineUnavailable if absent)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise EngineUnavailable(
+            f"{path} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            " (hipcc --offload-arch=gfx950). There is no CPU fallback.")
+    try:
+        lib = ctypes.CDLL(path)
+    except OSError as e:  # pragma: no cover - depends on the ROCm runtime
+        raise EngineUnavailable(f"cannot load {path}: {e}") from e
+    lib.pf_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+    lib.pf_ctx_destroy.argtypes = [vp]
+    lib.pf_last_error.argtypes = [vp]
+    lib.pf_last_error.restype = ctypes.c_char_p
+    lib.pf_default_fit_opts.argtypes = [ctypes.POINTER(PfFitOpts)]
+    lib.pf_default_fit_opts.restype = None
+    lib.pf_num_changepoints.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double]
+    lib.pf_build_grid.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64,
+                                  ctypes.c_int64, ctypes.POINTER(PfSeason), ctypes.c_int,
+                                  vp, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                  vp, vp, vp, vp, vp, vp, ctypes.c_int, vp]
+    lib.pf_prepare.argtypes = [vp, ctypes.c_int, ctypes.POINTER(PfGrid), ctypes.c_int,
+                               vp, vp, vp, vp, vp, vp, vp, vp]
+    lib.pf_objective_grad.argtypes = [vp, ctypes.POINTER(PfProblem), vp, vp, vp, vp]
+    lib.pf_fit.argtypes = [vp, ctypes.POINTER(PfProblem), ctypes.POINTER(PfFitOpts),
+                           vp, vp, vp, vp, vp, vp, vp]
+    lib.pf_predict.argtypes = [vp, ctypes.POINTER(PfPredictArgs), vp]
+    for name in EXPORTED:
+        if name not in ("pf_default_fit_opts",):
+            getattr(lib, name).restype = getattr(lib, name).restype or ctypes.c_int
+    _lib = lib
+    return lib
+
+
+def num_changepoints(T: int, n_changepoints: int = 25, changepoint_range: float = 0.8) -> int:
+    """pf_num_changepoints (pure host arithmetic, no GPU)."""
+    return int(load().pf_num_changepoints(int(T), int(n_changepoints), float(changepoint_range)))

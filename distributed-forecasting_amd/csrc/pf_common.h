@@ -1,0 +1,197 @@
+// pf_common.h — device-side helpers shared by the engine's HIP kernels (gfx950).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PF_WAVE 64
+
+// ---------------------------------------------------------------- wave math
+// All cross-lane traffic uses DPP / gfx950 permlane{16,32}_swap (VALU, a few
+// cycles) instead of __shfl (ds_bpermute: an LDS-unit round trip per step).
+// Callers must have all 64 lanes active.
+__device__ __forceinline__ int pf_lane() { return threadIdx.x & 63; }
+__device__ __forceinline__ int pf_wave() { return threadIdx.x >> 6; }
+
+// DPP controls (GFX9 encoding)
+#define PF_DPP_QXOR1 0xB1    // quad_perm [1,0,3,2]
+#define PF_DPP_QXOR2 0x4E    // quad_perm [2,3,0,1]
+#define PF_DPP_SHL(n) (0x100 + (n))
+#define PF_DPP_SHR(n) (0x110 + (n))
+#define PF_DPP_ROR(n) (0x120 + (n))
+#define PF_DPP_MIRROR 0x140
+#define PF_DPP_HMIRROR 0x141
+#define PF_DPP_BCAST15 0x142
+#define PF_DPP_BCAST31 0x143
+
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ int dpp_i32(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, ROW_MASK, 0xF, true);
+}
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __int_as_float(dpp_i32<CTRL, ROW_MASK>(__float_as_int(v)));
+}
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const int lo = dpp_i32<CTRL, ROW_MASK>((int)(unsigned)b);
+  const int hi = dpp_i32<CTRL, ROW_MASK>((int)(unsigned)(b >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = __builtin_amdgcn_readlane((int)(unsigned)b, l);
+  const unsigned hi = __builtin_amdgcn_readlane((int)(unsigned)(b >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ __forceinline__ float readlane_f32(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+// value of lane (lane ^ J), J in {1,2,4,8,16,32}
+template <int J>
+__device__ __forceinline__ float shfl_xor_f32(float x) {
+  if constexpr (J == 1) {
+    return dpp_f32<PF_DPP_QXOR1>(x);
+  } else if constexpr (J == 2) {
+    return dpp_f32<PF_DPP_QXOR2>(x);
+  } else if constexpr (J == 4) {
+    const float up = dpp_f32<PF_DPP_SHL(4)>(x);   // lane i <- i+4
+    const float dn = dpp_f32<PF_DPP_SHR(4)>(x);   // lane i <- i-4
+    return (pf_lane() & 4) ? dn : up;
+  } else if constexpr (J == 8) {
+    return dpp_f32<PF_DPP_ROR(8)>(x);             // within a row of 16: i ^ 8
+  } else if constexpr (J == 16) {
+    const unsigned u = __float_as_uint(x);
+    const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    return __uint_as_float((pf_lane() & 16) ? r[0] : r[1]);
+  } else {
+    static_assert(J == 32, "xor distance");
+    const unsigned u = __float_as_uint(x);
+    const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    return __uint_as_float((pf_lane() & 32) ? r[0] : r[1]);
+  }
+}
+template <int J>
+__device__ __forceinline__ double shfl_xor_f64(double x) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+  const float lo = shfl_xor_f32<J>(__uint_as_float((unsigned)b));
+  const float hi = shfl_xor_f32<J>(__uint_as_float((unsigned)(b >> 32)));
+  return __longlong_as_double((long long)(((unsigned long long)__float_as_uint(hi) << 32) |
+                                          __float_as_uint(lo)));
+}
+
+// full-wave sum, result uniform in every lane
+__device__ __forceinline__ double wave_sum(double v) {
+  v += dpp_f64<PF_DPP_QXOR1>(v);
+  v += dpp_f64<PF_DPP_QXOR2>(v);
+  v += dpp_f64<PF_DPP_HMIRROR>(v);
+  v += dpp_f64<PF_DPP_MIRROR>(v);
+  v += dpp_f64<PF_DPP_BCAST15, 0xA>(v);
+  v += dpp_f64<PF_DPP_BCAST31, 0xC>(v);
+  return readlane_f64(v, 63);
+}
+
+__device__ __forceinline__ float wave_minf(float v) {
+  v = fminf(v, shfl_xor_f32<1>(v));
+  v = fminf(v, shfl_xor_f32<2>(v));
+  v = fminf(v, shfl_xor_f32<4>(v));
+  v = fminf(v, shfl_xor_f32<8>(v));
+  v = fminf(v, shfl_xor_f32<16>(v));
+  v = fminf(v, shfl_xor_f32<32>(v));
+  return v;
+}
+
+// inclusive prefix sum across the wave (lane l gets sum_{l' <= l})
+__device__ __forceinline__ double wave_prefix_sum(double v) {
+  v += dpp_f64<PF_DPP_SHR(1)>(v);
+  v += dpp_f64<PF_DPP_SHR(2)>(v);
+  v += dpp_f64<PF_DPP_SHR(4)>(v);
+  v += dpp_f64<PF_DPP_SHR(8)>(v);
+  v += dpp_f64<PF_DPP_BCAST15, 0xA>(v);
+  v += dpp_f64<PF_DPP_BCAST31, 0xC>(v);
+  return v;
+}
+
+// value of lane l-1 (0 for lane 0): exclusive-scan helper
+__device__ __forceinline__ double wave_shift_up1(double v) {
+  // wave_shr:1 (0x138) is GFX8/9 only; gfx950 keeps it
+  return dpp_f64<0x138>(v);
+}
+
+// inclusive suffix sum (lane l gets sum_{l' >= l}); total returned in `tot`
+__device__ __forceinline__ double wave_suffix_sum(double v, double &tot) {
+  const double p = wave_prefix_sum(v);
+  tot = readlane_f64(p, 63);
+  return tot - p + v;
+}
+
+// ---------------------------------------------------------------- Philox4x32-10
+struct pf_u4 { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ pf_u4 philox4x32_10(pf_u4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    c = pf_u4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// uniform in (0,1) from 24 random bits (never 0, never 1)
+__device__ __forceinline__ float pf_u01f(uint32_t x) {
+  return ((float)(x >> 8) + 0.5f) * (1.0f / 16777216.0f);
+}
+// uniform in (0,1) in double from 53 bits of two words
+__device__ __forceinline__ double pf_u01d(uint32_t a, uint32_t b) {
+  const uint64_t v = ((uint64_t)a << 21) ^ (uint64_t)(b >> 11);
+  return ((double)(v & ((1ull << 53) - 1)) + 0.5) * (1.0 / 9007199254740992.0);
+}
+
+// Box-Muller: two normals from two uniforms (v_sin/v_cos take revolutions)
+__device__ __forceinline__ void pf_box_muller(float u1, float u2, float &z0, float &z1) {
+  const float r = __fsqrt_rn(-2.0f * __logf(u1));
+  z0 = r * __builtin_amdgcn_cosf(u2);
+  z1 = r * __builtin_amdgcn_sinf(u2);
+}
+
+// ---------------------------------------------------------------- bitonic sort across a wave (1 value / lane, ascending)
+template <int J>
+__device__ __forceinline__ float bitonic_step(float x, bool up) {
+  const float p = shfl_xor_f32<J>(x);
+  const bool lower = (pf_lane() & J) == 0;
+  return (lower == up) ? fminf(x, p) : fmaxf(x, p);
+}
+template <int K>
+__device__ __forceinline__ float bitonic_merge(float x) {
+  const bool up = (pf_lane() & K) == 0 || K == 64;
+  if constexpr (K >= 64) x = bitonic_step<32>(x, up);
+  if constexpr (K >= 32) x = bitonic_step<16>(x, up);
+  if constexpr (K >= 16) x = bitonic_step<8>(x, up);
+  if constexpr (K >= 8) x = bitonic_step<4>(x, up);
+  if constexpr (K >= 4) x = bitonic_step<2>(x, up);
+  x = bitonic_step<1>(x, up);
+  return x;
+}
+__device__ __forceinline__ float wave_bitonic_sort_asc(float x) {
+  x = bitonic_merge<2>(x);
+  x = bitonic_merge<4>(x);
+  x = bitonic_merge<8>(x);
+  x = bitonic_merge<16>(x);
+  x = bitonic_merge<32>(x);
+  x = bitonic_merge<64>(x);
+  return x;
+}
+
+__device__ __forceinline__ uint32_t pf_f2ord(float f) {
+  const uint32_t b = __float_as_uint(f);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float pf_ord2f(uint32_t o) {
+  return __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
+}

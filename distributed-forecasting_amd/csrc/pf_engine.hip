@@ -1,0 +1,1480 @@
+// pf_engine.hip — MI355X (gfx950) batched Prophet fit + forecast engine.
+//
+// Kernels:
+//   K1 k_grid_*      a1/a2/a3  t, Fourier features X^T, changepoints, segments
+//   -- k_prepare     a1/a4     y_scale, y_scaled, Prophet linear/flat init
+//   K2 k_objgrad     a5        Stan log-posterior (propto) + analytic gradient
+//   K3 k_fit         a6        Stan-faithful L-BFGS (+ exact-MAP polish, pf_polish.h)
+//   K4/K5 k_predict  a7/a8     point forecast + Poisson-process MC intervals
+//
+// One workgroup owns one series for the whole optimisation (persistent per
+// series): the series' y lives in LDS, every objective evaluation is a
+// collective pass over the rows (4 waves), and the L-BFGS state machine runs
+// redundantly in every wave (lane p holds parameter p), so the only
+// synchronisation is the handful of barriers inside each evaluation.
+// No CPU fallback exists: every entry point launches HIP kernels.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "pf_common.h"
+#include "prophet_hip.h"
+
+#ifndef M_PI
+#define M_PI 3.14159265358979323846
+#endif
+
+struct pf_ctx {
+  int device;
+  char err[512];
+};
+
+static char g_err_noctx[512] = "";
+
+static int set_err(pf_ctx *ctx, const char *msg) {
+  char *dst = ctx ? ctx->err : g_err_noctx;
+  snprintf(dst, 512, "%s", msg);
+  return -1;
+}
+
+#define PF_HIP(ctx, call)                                                        \
+  do {                                                                           \
+    hipError_t e_ = (call);                                                      \
+    if (e_ != hipSuccess) {                                                      \
+      char b_[480];                                                              \
+      snprintf(b_, sizeof b_, "%s failed: %s", #call, hipGetErrorString(e_));    \
+      set_err(ctx, b_);                                                          \
+      return -2;                                                                 \
+    }                                                                            \
+  } while (0)
+
+// ============================================================================
+// K1: design builder
+// ============================================================================
+#define PF_MAX_SEASONS 8
+struct SeasonSpec {
+  int n;
+  double period[PF_MAX_SEASONS];
+  int order[PF_MAX_SEASONS];
+};
+
+// t = (ds - start)/t_scale (numpy m8/m8 -> double/double);
+// d = (ns / 1e9) / 86400  (pandas total_seconds()/(3600*24.));
+// X col (2i, 2i+1) = sin, cos of ((2.0*(i+1))*pi*d)/period evaluated
+// left to right like UPSTREAM fourier_series.
+__global__ void k_grid_features(const int64_t *__restrict__ ds, int T, int Tp, int64_t start,
+                                int64_t tscale, SeasonSpec ss, const double *__restrict__ extra,
+                                int n_extra, double *__restrict__ t_out, double *__restrict__ XT) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= Tp) return;
+  int col = 0;
+  if (i >= T) {
+    if (t_out) t_out[i] = 0.0;
+    for (int b = 0; b < ss.n; ++b)
+      for (int r = 0; r < 2 * ss.order[b]; ++r) XT[(size_t)(col++) * Tp + i] = 0.0;
+    for (int e = 0; e < n_extra; ++e) XT[(size_t)(col++) * Tp + i] = 0.0;
+    return;
+  }
+  const int64_t ns = ds[i];
+  if (t_out) t_out[i] = __ddiv_rn((double)(ns - start), (double)tscale);
+  const double d = __ddiv_rn(__ddiv_rn((double)ns, 1e9), 86400.0);
+  for (int b = 0; b < ss.n; ++b) {
+    for (int r = 0; r < ss.order[b]; ++r) {
+      const double c = __dmul_rn(2.0 * (double)(r + 1), M_PI);
+      const double arg = __ddiv_rn(__dmul_rn(c, d), ss.period[b]);
+      double sn, cs;
+      sincos(arg, &sn, &cs);
+      XT[(size_t)(col++) * Tp + i] = sn;
+      XT[(size_t)(col++) * Tp + i] = cs;
+    }
+  }
+  for (int e = 0; e < n_extra; ++e) XT[(size_t)(col++) * Tp + i] = extra[(size_t)e * T + i];
+}
+
+// UPSTREAM set_changepoints: linspace(0, hist_size-1, n_cp+1).round()[1:]
+// (numpy: step = (stop-start)/div; y = arange*step; y[-1] = stop; rint)
+__global__ void k_grid_changepoints(const double *__restrict__ t, int T, int n_cp_req, double range,
+                                    double *__restrict__ t_change, int32_t *__restrict__ cp_idx) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const int hist_size = (int)floor((double)T * range);
+  int n_cp = n_cp_req;
+  if (n_cp + 1 > hist_size) n_cp = hist_size - 1;
+  if (n_cp > 0) {
+    const double stop = (double)(hist_size - 1);
+    const double step = stop / (double)n_cp;
+    for (int j = 1; j <= n_cp; ++j) {
+      const double v = (j == n_cp) ? stop : __dmul_rn((double)j, step);
+      const int idx = (int)rint(v);
+      cp_idx[j - 1] = idx;
+      t_change[j - 1] = t[idx];
+    }
+    // sort (stable insertion; already sorted for sorted t)
+    for (int a = 1; a < n_cp; ++a) {
+      double v = t_change[a];
+      int b = a - 1;
+      while (b >= 0 && t_change[b] > v) { t_change[b + 1] = t_change[b]; --b; }
+      t_change[b + 1] = v;
+    }
+  } else {
+    t_change[0] = 0.0;  // dummy changepoint, S = 1
+    cp_idx[0] = -1;
+  }
+}
+
+// seg[i] = #{j : t_change[j] <= t[i]} (Stan A[i,j] = t_i >= t_change_j);
+// cp_first[j] = first row with t >= t_change[j].
+__global__ void k_grid_segments(const double *__restrict__ t, int T, int Tp,
+                                const double *__restrict__ t_change, int S,
+                                int32_t *__restrict__ seg, int32_t *__restrict__ cp_first) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < Tp) {
+    int c = S;
+    if (i < T) {
+      const double ti = t[i];
+      c = 0;
+      for (int j = 0; j < S; ++j) c += (ti >= t_change[j]) ? 1 : 0;
+    }
+    seg[i] = c;
+  }
+  if (cp_first && i < S) {
+    const double tc = t_change[i];
+    int lo = 0, hi = T;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (t[mid] >= tc) hi = mid; else lo = mid + 1;
+    }
+    cp_first[i] = lo;
+  }
+}
+
+// ============================================================================
+// prepare: y_scale, y_scaled, init (UPSTREAM initialize_scales, *_growth_init)
+// ============================================================================
+__global__ __launch_bounds__(256) void k_prepare(int T, int Tp, const double *__restrict__ t,
+                                                 int growth, const double *__restrict__ y,
+                                                 double *__restrict__ y_scale,
+                                                 double *__restrict__ y_scaled,
+                                                 double *__restrict__ theta0,
+                                                 int32_t *__restrict__ status, int P, int S) {
+  __shared__ double red[3][4];
+  const int s = blockIdx.x;
+  const double *ys = y + (size_t)s * Tp;
+  double amax = 0.0, vmin = INFINITY, vmax = -INFINITY, vsum = 0.0;
+  for (int i = threadIdx.x; i < T; i += blockDim.x) {
+    const double v = ys[i];
+    amax = fmax(amax, fabs(v));
+    vmin = fmin(vmin, v);
+    vmax = fmax(vmax, v);
+  }
+  for (int o = 32; o >= 1; o >>= 1) {
+    amax = fmax(amax, __shfl_xor(amax, o, 64));
+    vmin = fmin(vmin, __shfl_xor(vmin, o, 64));
+    vmax = fmax(vmax, __shfl_xor(vmax, o, 64));
+  }
+  const int w = pf_wave(), lane = pf_lane();
+  if (lane == 0) { red[0][w] = amax; red[1][w] = vmin; red[2][w] = vmax; }
+  __syncthreads();
+  amax = fmax(fmax(red[0][0], red[0][1]), fmax(red[0][2], red[0][3]));
+  vmin = fmin(fmin(red[1][0], red[1][1]), fmin(red[1][2], red[1][3]));
+  vmax = fmax(fmax(red[2][0], red[2][1]), fmax(red[2][2], red[2][3]));
+  double scale = amax == 0.0 ? 1.0 : amax;
+  double *out = y_scaled + (size_t)s * Tp;
+  for (int i = threadIdx.x; i < Tp; i += blockDim.x) {
+    const double v = (i < T) ? ys[i] / scale : 0.0;
+    out[i] = v;
+    if (i < T) vsum += v;
+  }
+  vsum = wave_sum(vsum);
+  __syncthreads();
+  if (lane == 0) red[0][w] = vsum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    vsum = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    y_scale[s] = scale;
+    double *th = theta0 + (size_t)s * P;
+    for (int p = 0; p < P; ++p) th[p] = 0.0;
+    const double y0 = ys[0] / scale, y1 = ys[T - 1] / scale;
+    double k = 0.0, m = 0.0;
+    if (growth == PF_GROWTH_LINEAR) {
+      k = (y1 - y0) / (t[T - 1] - t[0]);
+      m = y0 - k * t[0];
+    } else if (growth == PF_GROWTH_FLAT) {
+      k = 0.0;
+      m = vsum / (double)T;
+    }
+    th[0] = k;
+    th[1] = m;
+    th[2 + S] = 0.0;  // log(sigma_obs = 1)
+    status[s] = (vmin == vmax && growth != PF_GROWTH_LOGISTIC) ? PF_ST_CONSTANT : 0;
+  }
+}
+
+// ============================================================================
+// K2/K3: objective + gradient (collective over one workgroup) and L-BFGS
+// ============================================================================
+enum { MODE_MULT = 0, MODE_ADD = 1, MODE_MIXED = 2 };
+
+struct FitKArgs {
+  int T, Tp, K, S, growth, P, NB;
+  const double *t, *XT, *t_change;
+  const int32_t *seg;
+  const double *sigmas, *s_a, *s_m;
+  double tau;
+  const double *y_scaled;
+  // fit
+  double *theta;
+  double *f_out, *f_stan, *g_out;
+  int32_t *status, *n_iter, *n_eval;
+  pf_fit_opts o;
+};
+
+// Generated Fourier block: harmonics r >= 1 from the first harmonic column
+// pair by the angle-addition recurrence (|err| ~ r ulp), so a pass reads two
+// columns per block instead of 2*order.
+template <int O, int OFF, int KMAX>
+__device__ __forceinline__ void gen_block(const double *__restrict__ XT, int Tp, int i,
+                                          double (&x)[KMAX]) {
+  if constexpr (O > 0) {
+    const double s1 = XT[(size_t)OFF * Tp + i];
+    const double c1 = XT[(size_t)(OFF + 1) * Tp + i];
+    x[OFF] = s1;
+    x[OFF + 1] = c1;
+    double sr = s1, cr = c1;
+#pragma unroll
+    for (int r = 1; r < O; ++r) {
+      const double sn = fma(sr, c1, cr * s1);
+      const double cn = fma(cr, c1, -(sr * s1));
+      sr = sn;
+      cr = cn;
+      x[OFF + 2 * r] = sr;
+      x[OFF + 2 * r + 1] = cr;
+    }
+  }
+}
+
+// Per-row inputs of one evaluation pass, loaded one batch ahead (prefetch).
+struct RowIn {
+  double t;
+  int seg, sprev;
+  double f[6];  // first-harmonic (sin, cos) of up to three Fourier blocks
+};
+
+template <int O0, int O1, int O2>
+__device__ __forceinline__ void load_row(const double *__restrict__ t, const int32_t *__restrict__ seg,
+                                         const double *__restrict__ XT, int Tp, int i, RowIn &r) {
+  r.t = t[i];
+  r.seg = seg[i];
+  r.sprev = (i == 0) ? 0 : seg[i - 1];
+  if constexpr (O0 > 0) { r.f[0] = XT[i]; r.f[1] = XT[(size_t)Tp + i]; }
+  if constexpr (O1 > 0) { r.f[2] = XT[(size_t)(2 * O0) * Tp + i]; r.f[3] = XT[(size_t)(2 * O0 + 1) * Tp + i]; }
+  if constexpr (O2 > 0) {
+    r.f[4] = XT[(size_t)(2 * (O0 + O1)) * Tp + i];
+    r.f[5] = XT[(size_t)(2 * (O0 + O1) + 1) * Tp + i];
+  }
+}
+
+template <int O, int OFF, int KMAX>
+__device__ __forceinline__ void gen_block_from(double s1, double c1, double (&x)[KMAX]) {
+  if constexpr (O > 0) {
+    x[OFF] = s1;
+    x[OFF + 1] = c1;
+    double sr = s1, cr = c1;
+#pragma unroll
+    for (int r = 1; r < O; ++r) {
+      const double sn = fma(sr, c1, cr * s1);
+      const double cn = fma(cr, c1, -(sr * s1));
+      sr = sn;
+      cr = cn;
+      x[OFF + 2 * r] = sr;
+      x[OFF + 2 * r + 1] = cr;
+    }
+  }
+}
+
+template <int KMAX, int O0, int O1, int O2>
+__device__ __forceinline__ void row_features_from(const RowIn &r, const double *__restrict__ XT,
+                                                  int Tp, int K, int i, double (&x)[KMAX]) {
+  constexpr int KF = 2 * (O0 + O1 + O2);
+  gen_block_from<O0, 0, KMAX>(r.f[0], r.f[1], x);
+  gen_block_from<O1, 2 * O0, KMAX>(r.f[2], r.f[3], x);
+  gen_block_from<O2, 2 * (O0 + O1), KMAX>(r.f[4], r.f[5], x);
+#pragma unroll
+  for (int f = KF; f < KMAX; ++f) x[f] = (f < K) ? XT[(size_t)f * Tp + i] : 0.0;
+}
+
+template <int KMAX, int O0, int O1, int O2>
+__device__ __forceinline__ void row_features(const double *__restrict__ XT, int Tp, int K, int i,
+                                             double (&x)[KMAX]) {
+  constexpr int KF = 2 * (O0 + O1 + O2);
+  gen_block<O0, 0, KMAX>(XT, Tp, i, x);
+  gen_block<O1, 2 * O0, KMAX>(XT, Tp, i, x);
+  gen_block<O2, 2 * (O0 + O1), KMAX>(XT, Tp, i, x);
+#pragma unroll
+  for (int f = KF; f < KMAX; ++f) x[f] = (f < K) ? XT[(size_t)f * Tp + i] : 0.0;
+}
+
+static constexpr size_t kLbBytes = 12 * 1024;
+struct LbLds;
+template <int NW, int KMAX>
+struct FitSmem {
+  double *y;        // [Tp]
+  double *th;       // [64]
+  double *kseg;     // [64]
+  double *mseg;     // [64]
+  double *bm, *ba;  // [KMAX]
+  double *bsum0, *bsum1;  // [NB]
+  double *cps0, *cps1;    // [64]
+  int *cpb;               // [64]
+  double *gbt;      // [NW][2][KMAX][64]
+  double *rrw;      // [NW]
+  double *gout;     // [64]
+  double *fout;     // [4]: f, bad
+  double *gb;       // [2][KMAX] reduced
+  struct LbLds *lb;
+  static __host__ __device__ size_t bytes(int Tp, int NB) {
+    return sizeof(double) * ((size_t)Tp + 64 * 3 + 2 * KMAX + 2 * (size_t)NB + 128 +
+                             (size_t)NW * 2 * KMAX * 64 + NW + 64 + 4 + 2 * KMAX) +
+           sizeof(int) * 64 + 64 + kLbBytes;
+  }
+  __device__ void carve(char *base, int Tp, int NB) {
+    double *p = reinterpret_cast<double *>(base);
+    y = p; p += Tp;
+    th = p; p += 64;
+    kseg = p; p += 64;
+    mseg = p; p += 64;
+    bm = p; p += KMAX;
+    ba = p; p += KMAX;
+    bsum0 = p; p += NB;
+    bsum1 = p; p += NB;
+    cps0 = p; p += 64;
+    cps1 = p; p += 64;
+    gbt = p; p += (size_t)NW * 2 * KMAX * 64;
+    rrw = p; p += NW;
+    gout = p; p += 64;
+    fout = p; p += 4;
+    gb = p; p += 2 * KMAX;
+    cpb = reinterpret_cast<int *>(p);
+    // align via offsets from the LDS base (an integer round trip would lose
+    // the address space and turn every access into a flat op)
+    size_t off = (size_t)(reinterpret_cast<char *>(cpb + 64) - base);
+    off = (off + 15) & ~(size_t)15;
+    lb = reinterpret_cast<struct LbLds *>(base + off);
+  }
+};
+
+// One collective evaluation of f(theta) = -log posterior and its gradient.
+// Every thread of the workgroup must call it.  `x` is this lane's parameter
+// (lane p < P); returns f in every thread and g (lane p) in `g`; returns true
+// if f or g is not finite (Stan ModelAdaptor error → line-search retreat).
+template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
+__device__ bool eval_collective(const FitKArgs &a, FitSmem<NW, KMAX> &sm, double x, double &f,
+                                double &g) {
+  const int lane = pf_lane(), wave = pf_wave();
+  const int P = a.P, S = a.S, K = a.K, T = a.T, Tp = a.Tp;
+  // ---- phase 0: wave 0 publishes theta and the segment rates/offsets
+  if (wave == 0) {
+    if (lane < P) sm.th[lane] = x;
+    const double k = readlane_f64(x, 0), m = readlane_f64(x, 1);
+    // delta_j sits in lane 2+j
+    const double dj = __shfl(x, (lane + 2) & 63, 64);
+    const double dval = (lane < S) ? dj : 0.0;
+    const double tcd = (lane < S) ? a.t_change[lane] * dval : 0.0;
+    const double cd = wave_prefix_sum(dval);   // inclusive: sum_{j<=lane}
+    const double ctd = wave_prefix_sum(tcd);
+    // kseg[s] = k + sum_{j<s} delta_j ; mseg[s] = m - sum_{j<s} tc_j delta_j
+    const double cd_ex = wave_shift_up1(cd);
+    const double ctd_ex = wave_shift_up1(ctd);
+    if (lane <= S) {
+      sm.kseg[lane] = k + (lane == 0 ? 0.0 : cd_ex);
+      sm.mseg[lane] = m - (lane == 0 ? 0.0 : ctd_ex);
+    }
+    const double bval = __shfl(x, (lane + 3 + S) & 63, 64);
+    if (lane < KMAX) {
+      const double bv = (lane < K) ? bval : 0.0;
+      sm.bm[lane] = bv * ((lane < K) ? a.s_m[lane] : 0.0);
+      sm.ba[lane] = bv * ((lane < K) ? a.s_a[lane] : 0.0);
+    }
+  }
+  __syncthreads();
+  // ---- phase 1: row pass (batch of 64 consecutive rows per wave iteration)
+  double gbm[KMAX], gba[KMAX];
+#pragma unroll
+  for (int f2 = 0; f2 < KMAX; ++f2) {
+    gbm[f2] = 0.0;
+    gba[f2] = 0.0;
+  }
+  const double *lbm = sm.bm;
+  const double *lba = sm.ba;
+  const double th_m = sm.th[1];
+  const bool linear = (a.growth == PF_GROWTH_LINEAR);
+  double rr = 0.0;
+  RowIn cur;
+  if (wave < a.NB) load_row<O0, O1, O2>(a.t, a.seg, a.XT, Tp, wave * 64 + lane, cur);
+  for (int b = wave; b < a.NB; b += NW) {
+    const int i = b * 64 + lane;
+    RowIn nxt;
+    if (b + NW < a.NB) load_row<O0, O1, O2>(a.t, a.seg, a.XT, Tp, (b + NW) * 64 + lane, nxt);
+    const bool valid = i < T;
+    const double ti = cur.t;
+    const int sg = cur.seg;
+    const int sprev = cur.sprev;
+    double xf[KMAX];
+    row_features_from<KMAX, O0, O1, O2>(cur, a.XT, Tp, K, i, xf);
+    double xm[4] = {0.0, 0.0, 0.0, 0.0}, xa[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int f2 = 0; f2 < KMAX; ++f2) {
+      if constexpr (MODE != MODE_ADD) xm[f2 & 3] = fma(xf[f2], lbm[f2], xm[f2 & 3]);
+      if constexpr (MODE != MODE_MULT) xa[f2 & 3] = fma(xf[f2], lba[f2], xa[f2 & 3]);
+      // stream the (uniform) coefficient loads in groups of 8 instead of
+      // letting the scheduler hoist all KMAX of them (register pressure)
+      if ((f2 & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+    }
+    const double xbm = (xm[0] + xm[1]) + (xm[2] + xm[3]);
+    const double xba = (xa[0] + xa[1]) + (xa[2] + xa[3]);
+    const double tr = linear ? fma(sm.kseg[sg], ti, sm.mseg[sg]) : th_m;
+    const double u = 1.0 + xbm;
+    const double mu = fma(tr, u, xba);
+    const double r = valid ? (sm.y[i] - mu) : 0.0;
+    rr = fma(r, r, rr);
+    const double G = r * u;
+    const double cm = r * tr;
+#pragma unroll
+    for (int f2 = 0; f2 < KMAX; ++f2) {
+      if constexpr (MODE != MODE_ADD) gbm[f2] = fma(xf[f2], cm, gbm[f2]);
+      if constexpr (MODE != MODE_MULT) gba[f2] = fma(xf[f2], r, gba[f2]);
+    }
+    // suffix sums of G and G*t inside the batch; batch totals + cp rows to LDS
+    double tot0, tot1;
+    const double s0 = wave_suffix_sum(G, tot0);
+    const double s1 = wave_suffix_sum(G * ti, tot1);
+    if (lane == 0) {
+      sm.bsum0[b] = tot0;
+      sm.bsum1[b] = tot1;
+    }
+    if (valid && sg > sprev) {
+      for (int j = sprev; j < sg; ++j) {
+        sm.cps0[j] = s0;
+        sm.cps1[j] = s1;
+        sm.cpb[j] = b;
+      }
+    }
+    cur = nxt;
+  }
+  // ---- phase 2: transpose-reduce the beta gradient partials through LDS
+  rr = wave_sum(rr);
+  if (lane == 0) sm.rrw[wave] = rr;
+  {
+    double *gw = sm.gbt + (size_t)wave * 2 * KMAX * 64;
+#pragma unroll
+    for (int f2 = 0; f2 < KMAX; ++f2) {
+      if constexpr (MODE != MODE_ADD) gw[f2 * 64 + lane] = gbm[f2];
+      if constexpr (MODE != MODE_MULT) gw[(KMAX + f2) * 64 + lane] = gba[f2];
+    }
+  }
+  __syncthreads();
+  {
+    // feature f handled by 8 threads, each summing NW*8 partials
+    constexpr int NSET = (MODE == MODE_MIXED) ? 2 : 1;
+    const int tid = threadIdx.x;
+    for (int job = tid; job < NSET * KMAX * 8; job += NW * 64) {
+      const int fs = job >> 3, part = job & 7;
+      const int set = (MODE == MODE_ADD) ? 1 : (fs / KMAX);
+      const int f2 = fs % KMAX;
+      double acc = 0.0;
+      for (int w2 = 0; w2 < NW; ++w2) {
+        const double *src = sm.gbt + ((size_t)w2 * 2 * KMAX + set * KMAX + f2) * 64 + part * 8;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc += src[q];
+      }
+      acc += shfl_xor_f64<1>(acc);
+      acc += shfl_xor_f64<2>(acc);
+      acc += shfl_xor_f64<4>(acc);
+      if (part == 0) sm.gb[set * KMAX + f2] = acc;
+    }
+  }
+  __syncthreads();
+  // ---- phase 3: wave 0 assembles f and g
+  if (wave == 0) {
+    double rrt = 0.0;
+    for (int w2 = 0; w2 < NW; ++w2) rrt += sm.rrw[w2];
+    // BS[b] = sum_{b' >= b} bsum[b'] (lane = batch when NB <= 64)
+    double tot0, tot1, BS0 = 0.0, BS1 = 0.0;
+    if (a.NB <= 64) {
+      const double v0 = (lane < a.NB) ? sm.bsum0[lane] : 0.0;
+      const double v1 = (lane < a.NB) ? sm.bsum1[lane] : 0.0;
+      BS0 = wave_suffix_sum(v0, tot0);
+      BS1 = wave_suffix_sum(v1, tot1);
+    } else {
+      double l0 = 0.0, l1 = 0.0;
+      for (int bb = lane; bb < a.NB; bb += 64) { l0 += sm.bsum0[bb]; l1 += sm.bsum1[bb]; }
+      tot0 = wave_sum(l0);
+      tot1 = wave_sum(l1);
+    }
+    const double ls = readlane_f64(x, 2 + S);
+    const double sigma = exp(ls);
+    const double inv_s2 = 1.0 / (sigma * sigma);
+    // SU_j (at lane 2+j): cps_j + sum of the batches after cp j's batch
+    double gdel = 0.0;
+    {
+      const int j = lane - 2;  // delta_j lives at lane 2+j
+      const bool has = (j >= 0 && j < S);
+      const int bj1 = has ? sm.cpb[j] + 1 : 63;
+      double later0, later1;
+      if (a.NB <= 64) {
+        // gather BS[bj+1] (0 past the end): one bpermute per evaluation
+        const double g0 = __shfl(BS0, bj1 & 63, 64), g1 = __shfl(BS1, bj1 & 63, 64);
+        later0 = (bj1 < a.NB) ? g0 : 0.0;
+        later1 = (bj1 < a.NB) ? g1 : 0.0;
+      } else {
+        later0 = later1 = 0.0;
+        if (has)
+          for (int bb = bj1; bb < a.NB; ++bb) { later0 += sm.bsum0[bb]; later1 += sm.bsum1[bb]; }
+      }
+      if (has) {
+        const double su0 = sm.cps0[j] + later0;
+        const double su1 = sm.cps1[j] + later1;
+        gdel = su1 - a.t_change[j] * su0;
+      }
+    }
+    double gv = 0.0, fterm = 0.0;
+    const int p = lane;
+    if (p == 0) {
+      const double k = x;
+      gv = (linear ? -inv_s2 * tot1 : 0.0) + k / 25.0;
+      fterm = k * k / 50.0;
+    } else if (p == 1) {
+      const double m = x;
+      gv = -inv_s2 * tot0 + m / 25.0;
+      fterm = m * m / 50.0;
+    }
+    const double gd_here = gdel;
+    if (p >= 2 && p < 2 + S) {
+      const double d = x;
+      const double sg = (d > 0.0) - (d < 0.0);
+      gv = (linear ? -inv_s2 * gd_here : 0.0) + sg / a.tau;
+      fterm = fabs(d) / a.tau;
+    } else if (p == 2 + S) {
+      gv = (double)T - inv_s2 * rrt + 4.0 * sigma * sigma;
+      fterm = 2.0 * sigma * sigma + (double)T * ls;
+    } else if (p > 2 + S && p < P) {
+      const int f2 = p - 3 - S;
+      const double bv = x;
+      const double sgm = a.sigmas[f2];
+      double gl = 0.0;
+      if (MODE != MODE_ADD) gl += a.s_m[f2] * sm.gb[f2];
+      if (MODE != MODE_MULT) gl += a.s_a[f2] * sm.gb[KMAX + f2];
+      gv = -inv_s2 * gl + bv / (sgm * sgm);
+      fterm = bv * bv / (2.0 * sgm * sgm);
+    }
+    const double fsum = wave_sum(fterm) + 0.5 * rrt * inv_s2;
+    bool bad = !isfinite(fsum);
+    if (p < P && !isfinite(gv)) bad = true;
+    const unsigned long long anybad = __ballot(bad);
+    if (p < 64) sm.gout[p] = (p < P) ? gv : 0.0;
+    if (lane == 0) {
+      sm.fout[0] = fsum;
+      sm.fout[1] = anybad ? 1.0 : 0.0;
+    }
+  }
+  __syncthreads();
+  f = sm.fout[0];
+  g = sm.gout[lane];
+  const bool bad = sm.fout[1] != 0.0;
+  __syncthreads();
+  return bad;
+}
+
+template <int NW, int KMAX>
+__device__ __forceinline__ void load_y(const FitKArgs &a, FitSmem<NW, KMAX> &sm, int s) {
+  const double *ys = a.y_scaled + (size_t)s * a.Tp;
+  for (int i = threadIdx.x; i < a.Tp; i += NW * 64) sm.y[i] = ys[i];
+}
+
+// ---------------------------------------------------------------- K2 kernel
+template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
+__global__ __launch_bounds__(NW * 64) void k_objgrad(FitKArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  FitSmem<NW, KMAX> sm;
+  sm.carve(smem_raw, a.Tp, a.NB);
+  const int s = blockIdx.x, lane = pf_lane();
+  load_y(a, sm, s);
+  const double x = (lane < a.P) ? a.theta[(size_t)s * a.P + lane] : 0.0;
+  __syncthreads();
+  double f, g;
+  const bool bad = eval_collective<NW, KMAX, O0, O1, O2, MODE>(a, sm, x, f, g);
+  if (threadIdx.x < 64) {
+    if (lane < a.P) a.g_out[(size_t)s * a.P + lane] = g;
+    if (lane == 0) a.f_out[s] = bad ? NAN : f;
+  }
+}
+
+// ---------------------------------------------------------------- L-BFGS (Stan 2.19 restatement)
+__device__ __forceinline__ double cubic_interp0(double df0, double x1, double f1, double df1,
+                                                double loX, double hiX) {
+  const double c3 = (-12 * f1 + 6 * x1 * (df0 + df1)) / (x1 * x1 * x1);
+  const double c2 = -(4 * df0 + 2 * df1) / x1 + 6 * f1 / (x1 * x1);
+  const double c1 = df0;
+  const double t_s = sqrt(c2 * c2 - 2.0 * c1 * c3);
+  const double s1 = -(c2 + t_s) / c3;
+  const double s2 = -(c2 - t_s) / c3;
+  double tmpF, minF, minX;
+  minF = loX * (loX * (loX * c3 / 3.0 + c2) / 2.0 + c1);
+  minX = loX;
+  tmpF = hiX * (hiX * (hiX * c3 / 3.0 + c2) / 2.0 + c1);
+  if (tmpF < minF) { minF = tmpF; minX = hiX; }
+  if (loX < s1 && s1 < hiX) {
+    tmpF = s1 * (s1 * (s1 * c3 / 3.0 + c2) / 2.0 + c1);
+    if (tmpF < minF) { minF = tmpF; minX = s1; }
+  }
+  if (loX < s2 && s2 < hiX) {
+    tmpF = s2 * (s2 * (s2 * c3 / 3.0 + c2) / 2.0 + c1);
+    if (tmpF < minF) { minF = tmpF; minX = s2; }
+  }
+  return minX;
+}
+
+__device__ __forceinline__ double cubic_interp(double x0, double f0, double df0, double x1,
+                                               double f1, double df1, double loX, double hiX) {
+  return x0 + cubic_interp0(df0, x1 - x0, f1 - f0, df1, loX - x0, hiX - x0);
+}
+
+#define PF_HIST 5
+
+// Reverse-communication restatement of Stan's BFGSMinimizer<LBFGSUpdate>::step
+// + WolfeLineSearch + WolfLSZoom (same control flow as oracle/stan_lbfgs.c),
+// written as a state machine so that the collective evaluation has exactly
+// one call site (keeps the workgroup's register budget at 2+ waves/SIMD).
+// All waves run it redundantly; vectors are one parameter per lane.
+enum LbState {
+  LB_INIT = 0, LB_NEW_ITER, LB_LS_START, LB_TRY, LB_TRY_RES, LB_ZOOM_ITER, LB_ZOOM_RES,
+  LB_LS_FAIL, LB_LS_OK, LB_DONE
+};
+
+struct LbScalars {
+  double fk, fk1, fq, alpha, alphak_1, gammak;
+  double dfp, c1dfp, c2dfp, alpha0, alpha1, prevF, prevDFp;
+  double alo, aloF, aloDFp, ahi, ahiF, ahiDFp;
+  int itNum, resetB, nits, lsRestarts, zit, hcount, ret, n_eval;
+};
+
+__device__ __forceinline__ double ddot(double u, double v) { return wave_sum(u * v); }
+
+// Optimizer state kept in LDS (wave 0 only) so it does not compete with the
+// evaluation's registers.
+struct LbLds {
+  double xk[64], gk[64], pk[64], xk1[64], gk1[64], pk1[64];
+  double hs[PF_HIST][64], hy[PF_HIST][64];
+  double hrho[PF_HIST];
+  LbScalars z;
+  int state;
+  int need;
+};
+
+// Advance the machine until it needs an evaluation (returns true, trial point
+// in xq) or terminates (returns false).  `bad` / fq / gq are the result of the
+// evaluation requested last time.
+__device__ __forceinline__ bool lbfgs_advance(const pf_fit_opts &o, LbLds &L, double &xq, double gq, bool bad) {
+  const int lane = pf_lane();
+  const int H = o.history < PF_HIST ? o.history : PF_HIST;
+  int &state = L.state;
+  LbScalars &z = L.z;
+  double &xk = L.xk[lane], &gk = L.gk[lane], &pk = L.pk[lane];
+  double &xk1 = L.xk1[lane], &gk1 = L.gk1[lane], &pk1 = L.pk1[lane];
+  double *hrho = L.hrho;
+  while (true) {
+    switch (state) {
+      case LB_INIT:
+        if (bad) { z.ret = PF_ST_BADINIT; state = LB_DONE; return false; }
+        z.fk = z.fq;
+        gk = gq;
+        pk = -gk;
+        z.itNum = 0;
+        state = LB_NEW_ITER;
+        break;
+      case LB_NEW_ITER:
+        z.itNum++;
+        z.resetB = (z.itNum == 1) ? 1 : 0;
+        state = LB_LS_START;
+        break;
+      case LB_LS_START:
+        if (z.resetB) pk = -gk;
+        if (z.itNum > 1 && z.resetB != 2) {
+          z.alpha = fmin(1.0, 1.01 * cubic_interp0(ddot(gk1, pk1), z.alphak_1, z.fk - z.fk1,
+                                                   ddot(gk, pk1), 1e-12, 1.0));
+        } else {
+          z.alpha = o.init_alpha;
+        }
+        z.dfp = ddot(gk, pk);
+        z.c1dfp = 1e-4 * z.dfp;
+        z.c2dfp = 0.9 * z.dfp;
+        z.alpha0 = 1e-12;
+        z.alpha1 = z.alpha;
+        z.prevF = z.fk;
+        z.prevDFp = z.dfp;
+        z.nits = 0;
+        z.lsRestarts = 0;
+        state = LB_TRY;
+        break;
+      case LB_TRY:
+        if (z.nits >= 20) { state = LB_LS_FAIL; break; }
+        xq = xk + z.alpha1 * pk;
+        state = LB_TRY_RES;
+        return true;
+      case LB_TRY_RES: {
+        if (bad) {
+          if (z.lsRestarts >= 10) { state = LB_LS_FAIL; break; }
+          z.alpha1 = 0.5 * (z.alpha0 + z.alpha1);
+          z.lsRestarts++;
+          state = LB_TRY;
+          break;
+        }
+        z.lsRestarts = 0;
+        const double f1 = z.fq;
+        const double newDFp = ddot(gq, pk);
+        if ((f1 > z.fk + z.alpha1 * z.c1dfp) || (f1 >= z.prevF && z.nits > 0)) {
+          z.alo = z.alpha0; z.aloF = z.prevF; z.aloDFp = z.prevDFp;
+          z.ahi = z.alpha1; z.ahiF = f1; z.ahiDFp = newDFp;
+          z.zit = 0;
+          state = LB_ZOOM_ITER;
+        } else if (fabs(newDFp) <= -z.c2dfp) {
+          z.alpha = z.alpha1;
+          state = LB_LS_OK;
+        } else if (newDFp >= 0) {
+          z.alo = z.alpha1; z.aloF = f1; z.aloDFp = newDFp;
+          z.ahi = z.alpha0; z.ahiF = z.prevF; z.ahiDFp = z.prevDFp;
+          z.zit = 0;
+          state = LB_ZOOM_ITER;
+        } else {
+          z.alpha0 = z.alpha1;
+          z.prevF = f1;
+          z.prevDFp = newDFp;
+          z.alpha1 *= 10.0;
+          z.nits++;
+          state = LB_TRY;
+        }
+        break;
+      }
+      case LB_ZOOM_ITER: {
+        z.zit++;
+        if (fabs(z.alo - z.ahi) < 1e-16) { state = LB_LS_FAIL; break; }
+        if (z.zit % 5 == 0) {
+          z.alpha = 0.5 * (z.alo + z.ahi);
+        } else {
+          const double lo = fmin(z.alo, z.ahi), hi = fmax(z.alo, z.ahi);
+          z.alpha = cubic_interp(z.alo, z.aloF, z.aloDFp, z.ahi, z.ahiF, z.ahiDFp, lo, hi);
+          if (z.alpha < lo + 0.01 * (hi - lo) || z.alpha > hi - 0.01 * (hi - lo))
+            z.alpha = 0.5 * (z.alo + z.ahi);
+        }
+        xq = xk + z.alpha * pk;
+        state = LB_ZOOM_RES;
+        return true;
+      }
+      case LB_ZOOM_RES: {
+        if (bad) {
+          const double lo = fmin(z.alo, z.ahi);
+          z.alpha = 0.5 * (z.alpha + lo);
+          if (fabs(lo - z.alpha) < 1e-16) { state = LB_LS_FAIL; break; }
+          xq = xk + z.alpha * pk;
+          return true;  // stay in LB_ZOOM_RES
+        }
+        const double f1 = z.fq;
+        const double newDFp = ddot(gq, pk);
+        if (f1 > (z.fk + z.alpha * z.c1dfp) || f1 >= z.aloF) {
+          z.ahi = z.alpha; z.ahiF = f1; z.ahiDFp = newDFp;
+          state = LB_ZOOM_ITER;
+        } else {
+          if (fabs(newDFp) <= -z.c2dfp) { state = LB_LS_OK; break; }
+          if (newDFp * (z.ahi - z.alo) >= 0) { z.ahi = z.alo; z.ahiF = z.aloF; z.ahiDFp = z.aloDFp; }
+          z.alo = z.alpha; z.aloF = f1; z.aloDFp = newDFp;
+          state = LB_ZOOM_ITER;
+        }
+        break;
+      }
+      case LB_LS_FAIL:
+        if (z.resetB) { z.ret = PF_ST_LSFAIL; state = LB_DONE; return false; }
+        z.resetB = 2;
+        state = LB_LS_START;
+        break;
+      case LB_LS_OK: {
+        // accepted point = last evaluated (xq, fq, gq); swap so k is the newest
+        z.fk1 = z.fk;
+        z.fk = z.fq;
+        xk1 = xk; xk = xq;
+        gk1 = gk; gk = gq;
+        pk1 = pk;
+        const double sk = xk - xk1, yk = gk - gk1;
+        z.alphak_1 = z.alpha;
+        if (fabs(z.fk1 - z.fk) < o.tol_obj) {
+          z.ret = PF_ST_ABSF;
+        } else if (sqrt(ddot(gk, gk)) < o.tol_grad) {
+          z.ret = PF_ST_ABSGRAD;
+        } else if (sqrt(ddot(sk, sk)) < o.tol_param) {
+          z.ret = PF_ST_ABSX;
+        } else if (z.itNum >= o.max_iter) {
+          z.ret = PF_ST_MAXIT;
+        } else if (((z.fk1 - z.fk) / fmax(fabs(z.fk1), fmax(fabs(z.fk), 1.0))) <
+                   o.tol_rel_obj * 2.220446049250313e-16) {
+          z.ret = PF_ST_RELF;
+        } else {
+          const double skyk = ddot(yk, sk);
+          if (z.resetB) z.hcount = 0;
+          z.gammak = skyk / ddot(yk, yk);
+          if (z.hcount == H) {
+#pragma unroll
+            for (int q = 0; q < PF_HIST - 1; ++q)
+              if (q < H - 1) {
+                L.hs[q][lane] = L.hs[q + 1][lane];
+                L.hy[q][lane] = L.hy[q + 1][lane];
+                if (lane == 0) hrho[q] = hrho[q + 1];
+              }
+            z.hcount = H - 1;
+          }
+#pragma unroll
+          for (int q = 0; q < PF_HIST; ++q)
+            if (q == z.hcount) {
+              L.hs[q][lane] = sk;
+              L.hy[q][lane] = yk;
+              if (lane == 0) hrho[q] = 1.0 / skyk;
+            }
+          z.hcount++;
+          double al[PF_HIST];
+          pk = -gk;
+#pragma unroll
+          for (int q = PF_HIST - 1; q >= 0; --q) {
+            al[q] = 0.0;
+            if (q < z.hcount) {
+              al[q] = hrho[q] * ddot(L.hs[q][lane], pk);
+              pk -= al[q] * L.hy[q][lane];
+            }
+          }
+          pk *= z.gammak;
+#pragma unroll
+          for (int q = 0; q < PF_HIST; ++q) {
+            if (q < z.hcount) {
+              const double bq = hrho[q] * ddot(L.hy[q][lane], pk);
+              pk += (al[q] - bq) * L.hs[q][lane];
+            }
+          }
+          if (-ddot(pk, gk) / fmax(fabs(z.fk), 1.0) < o.tol_rel_grad * 2.220446049250313e-16)
+            z.ret = PF_ST_RELGRAD;
+          else
+            z.ret = PF_ST_SUCCESS;
+        }
+        if (z.ret != PF_ST_SUCCESS) { state = LB_DONE; return false; }
+        state = LB_NEW_ITER;
+        break;
+      }
+      default:
+        return false;
+    }
+  }
+}
+
+static_assert(sizeof(LbLds) + 16 <= kLbBytes, "LbLds too big");
+
+#include "pf_polish.h"
+
+// ---------------------------------------------------------------- K3 kernel
+template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
+__global__ __launch_bounds__(NW * 64, 2) void k_fit(FitKArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  FitSmem<NW, KMAX> sm;
+  sm.carve(smem_raw, a.Tp, a.NB);
+  const int s = blockIdx.x, lane = pf_lane();
+  const int P = a.P;
+  double *th_out = a.theta + (size_t)s * P;
+  const int st_in = a.status[s];
+  if (st_in == PF_ST_CONSTANT) {
+    // Prophet: params = init, sigma_obs = 1e-9; optimizer skipped
+    if (threadIdx.x == 0) {
+      th_out[2 + a.S] = log(1e-9);
+      a.f_out[s] = NAN;
+      a.f_stan[s] = NAN;
+      a.n_iter[s] = 0;
+      a.n_eval[s] = 0;
+    }
+    return;
+  }
+  load_y(a, sm, s);
+  LbLds &L = *sm.lb;
+  double xq = (lane < P) ? th_out[lane] : 0.0;
+  if (pf_wave() == 0) {
+    L.state = LB_INIT;
+    L.xk[lane] = xq;
+    if (lane == 0) memset(&L.z, 0, sizeof(LbScalars));
+#pragma unroll
+    for (int q = 0; q < PF_HIST; ++q) { L.hs[q][lane] = 0.0; L.hy[q][lane] = 0.0; }
+    if (lane < PF_HIST) L.hrho[lane] = 0.0;
+  }
+  __syncthreads();
+  // ---- phase A: Stan-faithful L-BFGS (reverse communication)
+  int n_eval = 0;
+  while (true) {
+    double fq, gq;
+    const bool bad = eval_collective<NW, KMAX, O0, O1, O2, MODE>(a, sm, xq, fq, gq);
+    ++n_eval;
+    if (pf_wave() == 0) {
+      L.z.fq = fq;
+      const bool need = lbfgs_advance(a.o, L, xq, gq, bad);
+      if (lane == 0) L.need = need ? 1 : 0;
+    }
+    __syncthreads();
+    const int need = L.need;
+    __syncthreads();
+    if (!need) break;
+  }
+  double xk = L.xk[lane];
+  double gk = L.gk[lane];
+  double f = L.z.fk;
+  const double f_stan = f;
+  // ---- phase B: exact-MAP polish (engine extension, see pf_polish.h)
+  if (a.o.polish && L.z.ret != PF_ST_BADINIT && a.growth == PF_GROWTH_LINEAR) {
+    polish_run<NW, KMAX, O0, O1, O2, MODE>(a, sm, xk, f, gk, n_eval);
+  }
+  if (threadIdx.x < 64) {
+    if (lane < P) th_out[lane] = xk;
+    if (lane == 0) {
+      a.f_out[s] = f;
+      a.f_stan[s] = f_stan;
+      a.status[s] = L.z.ret;
+      a.n_iter[s] = L.z.itNum;
+      a.n_eval[s] = n_eval;
+    }
+  }
+}
+
+// ============================================================================
+// K4+K5: forecast + Monte-Carlo uncertainty (UPSTREAM predict / 0.7.1-1.0
+//        sample_predictive_trend Poisson process / nanpercentile 'linear')
+// ============================================================================
+#define PF_NQ 16  // samples per lane (n_samples <= 1024)
+
+struct PredKArgs {
+  int n_series, growth, N, Tf, Tp, K, S, P;
+  const double *t, *XT, *t_change;
+  const int32_t *seg;
+  const double *s_a, *s_m;
+  const double *theta, *y_scale;
+  double t_max, lam_pois;
+  int k_lo, k_hi_neg;  // order statistics: lower k_lo,k_lo+1; upper via negation
+  float fr_lo, fr_hi;
+  uint32_t seed0, seed1;
+  float *yhat, *ylo, *yhi, *tr, *trlo, *trhi, *mult, *add;
+};
+
+// k-th and (k+1)-th smallest of the wave's samples (v[q] = +inf if absent).
+// Fast path: bound from the (k+2)-th smallest per-lane minimum, compact the
+// candidates into LDS, bitonic-sort 64.  Fallback: exact bit-bisection.
+__device__ __noinline__ void wave_select_pair(const float (&v)[PF_NQ], int k, float *buf, float &a, float &b) {
+  const int lane = pf_lane();
+  float lmin = INFINITY;
+#pragma unroll
+  for (int q = 0; q < PF_NQ; ++q) lmin = fminf(lmin, v[q]);
+  int M = 1 << 30;
+  if (k + 1 < 63) {
+    const float srt = wave_bitonic_sort_asc(lmin);
+    const float U = readlane_f32(srt, k + 1);
+    int base = 0;
+    const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
+    for (int q = 0; q < PF_NQ; ++q) {
+      const bool pr = v[q] <= U;
+      const unsigned long long m = __ballot(pr);
+      if (pr) {
+        const int pos = base + __popcll(m & lt);
+        if (pos < 64) buf[pos] = v[q];
+      }
+      base += __popcll(m);
+    }
+    M = base;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (M <= 64) {
+      float c = (lane < M) ? buf[lane] : INFINITY;
+      c = wave_bitonic_sort_asc(c);
+      a = readlane_f32(c, k);
+      b = readlane_f32(c, k + 1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (M > 64) {
+    uint32_t key[PF_NQ];
+#pragma unroll
+    for (int q = 0; q < PF_NQ; ++q) key[q] = pf_f2ord(v[q]);
+    for (int want = 0; want < 2; ++want) {
+      const int kk = k + want;
+      uint32_t lo = 0u, hi = 0xFFFFFFFFu;
+      while (lo < hi) {
+        const uint32_t mid = lo + ((hi - lo) >> 1);
+        int cnt = 0;
+#pragma unroll
+        for (int q = 0; q < PF_NQ; ++q) cnt += __popcll(__ballot(key[q] <= mid));
+        if (cnt >= kk + 1) hi = mid; else lo = mid + 1;
+      }
+      if (want == 0) a = pf_ord2f(lo); else b = pf_ord2f(lo);
+    }
+  }
+}
+
+// numpy _lerp: a + (b-a)*t, or b - (b-a)*(1-t) when t >= 0.5
+__device__ __forceinline__ float np_lerp(float a, float b, float t) {
+  const float d = b - a;
+  return (t >= 0.5f) ? (b - d * (1.0f - t)) : (a + d * t);
+}
+
+// trend offset of MC sample `smp` at time ti (in scaled units):
+// sum over the sample's new changepoints with ti >= t_c of delta_c (ti - t_c)
+__device__ __noinline__ double mc_trend_offset(const PredKArgs &a, int series, int smp,
+                                                  double ti, double lam) {
+  const pf_u4 r0 = philox4x32_10(pf_u4{(uint32_t)smp, 0u, (uint32_t)series, 0x7EE2D00Du},
+                                 a.seed0 ^ 0x5A5A5A5Au, a.seed1);
+  // Poisson(lam_pois) by inversion
+  const double u0 = pf_u01d(r0.x, r0.y);
+  int n = 0;
+  if (a.lam_pois > 0.0) {
+    double p = exp(-a.lam_pois), F = p;
+    while (u0 > F && n < 100000) {
+      ++n;
+      p *= a.lam_pois / (double)n;
+      F += p;
+      if (p == 0.0 && F < u0) break;
+    }
+  }
+  double off = 0.0;
+  for (int c = 0; c < n; ++c) {
+    const pf_u4 rc = philox4x32_10(pf_u4{(uint32_t)smp, (uint32_t)(c + 1), (uint32_t)series,
+                                         0x7EE2D00Du},
+                                   a.seed0 ^ 0x5A5A5A5Au, a.seed1);
+    const double tc = 1.0 + pf_u01d(rc.x, rc.y) * (a.t_max - 1.0);
+    const double ul = pf_u01d(rc.z, rc.w);
+    const double lap = (ul >= 0.5) ? -lam * log(2.0 - ul - ul) : lam * log(ul + ul);
+    if (ti >= tc) off += lap * (ti - tc);
+  }
+  return off;
+}
+
+template <int KMAX, int MODE>
+__global__ __launch_bounds__(256) void k_predict(PredKArgs a) {
+  // (a is a by-value copy: t_max / lam_pois are filled in below)
+  __shared__ double s_kseg[64], s_mseg[64], s_bm[64], s_ba[64], s_sc[4];
+  __shared__ float s_buf[4][64];
+  __shared__ float s_off[4][64 * PF_NQ];
+  const int series = blockIdx.y, lane = pf_lane(), wave = pf_wave();
+  const int P = a.P, S = a.S, K = a.K;
+  if (wave == 0) {
+    const double x = (lane < P) ? a.theta[(size_t)series * P + lane] : 0.0;
+    const double k = readlane_f64(x, 0), m = readlane_f64(x, 1);
+    const double dj = __shfl(x, (lane + 2) & 63, 64);
+    const double dval = (lane < S) ? dj : 0.0;
+    const double tcd = (lane < S) ? a.t_change[lane] * dval : 0.0;
+    const double cd = wave_prefix_sum(dval), ctd = wave_prefix_sum(tcd);
+    const double cd_ex = wave_shift_up1(cd), ctd_ex = wave_shift_up1(ctd);
+    if (lane <= S) {
+      s_kseg[lane] = k + (lane == 0 ? 0.0 : cd_ex);
+      s_mseg[lane] = m - (lane == 0 ? 0.0 : ctd_ex);
+    }
+    const double bval = __shfl(x, (lane + 3 + S) & 63, 64);
+    const double bv = (lane < K) ? bval : 0.0;
+    s_bm[lane] = bv * ((lane < K) ? a.s_m[lane] : 0.0);
+    s_ba[lane] = bv * ((lane < K) ? a.s_a[lane] : 0.0);
+    const double absd = wave_sum(fabs(dval));
+    const double ls = readlane_f64(x, 2 + S);
+    if (lane == 0) {
+      s_sc[0] = exp(ls);                            // sigma_obs
+      s_sc[1] = a.y_scale[series];
+      s_sc[2] = absd / (double)S + 1e-8;            // lambda = mean|delta| + 1e-8
+    }
+  }
+  __syncthreads();
+  const double sigma = s_sc[0], ysc = s_sc[1], lam = s_sc[2];
+  const bool linear = a.growth == PF_GROWTH_LINEAR;
+  // UPSTREAM sample_predictive_trend: T = t.max() of the frame being predicted
+  // (rows sorted, so the last valid row); Poisson rate S*(T-1) when T > 1.
+  a.t_max = a.t[a.Tf - 1];
+  a.lam_pois = (a.t_max > 1.0) ? (double)S * (a.t_max - 1.0) : 0.0;
+  for (int r = 0; r < 4; ++r) {
+    const int row = blockIdx.x * 16 + wave * 4 + r;
+    if (row >= a.Tf) break;
+    const double ti = a.t[row];
+    const int sg = a.seg[row];
+    double xbm = 0.0, xba = 0.0;
+    if (lane < K) {
+      const double xv = a.XT[(size_t)lane * a.Tp + row];
+      xbm = xv * s_bm[lane];
+      xba = xv * s_ba[lane];
+    }
+    xbm = wave_sum(xbm);
+    xba = wave_sum(xba);
+    const double trs = linear ? (s_kseg[sg] * ti + s_mseg[sg]) : s_mseg[0];
+    const double trend = trs * ysc;
+    const double addt = xba * ysc;
+    const double yhat = trend * (1.0 + xbm) + addt;
+    float ylo = (float)yhat, yhi = (float)yhat, tlo = (float)trend, thi = (float)trend;
+    if (a.N > 0) {
+      float z[PF_NQ];
+#pragma unroll
+      for (int c = 0; c < PF_NQ / 4; ++c) {
+        const pf_u4 rr = philox4x32_10(pf_u4{(uint32_t)c, (uint32_t)lane, (uint32_t)row,
+                                              (uint32_t)series},
+                                       a.seed0, a.seed1);
+        pf_box_muller(pf_u01f(rr.x), pf_u01f(rr.y), z[4 * c + 0], z[4 * c + 1]);
+        pf_box_muller(pf_u01f(rr.z), pf_u01f(rr.w), z[4 * c + 2], z[4 * c + 3]);
+      }
+      const float sd = (float)(sigma * ysc);
+      const float u1 = (float)(1.0 + xbm);
+      const float addf = (float)addt;
+      float v[PF_NQ], tv[PF_NQ];
+      const bool future = linear && (ti > 1.0) && (a.t_max > 1.0);
+      if (!future) {
+        const float base = (float)yhat;
+#pragma unroll
+        for (int q = 0; q < PF_NQ; ++q) {
+          const int smp = lane + 64 * q;
+          v[q] = (smp < a.N) ? fmaf(sd, z[q], base) : INFINITY;
+        }
+      } else {
+        // per-sample trend offsets (rolled loop; keeps the code small)
+        float *offs = s_off[wave];
+#pragma unroll 1
+        for (int q = 0; q < PF_NQ; ++q) {
+          const int smp = lane + 64 * q;
+          offs[q * 64 + lane] = (smp < a.N) ? (float)(ysc * mc_trend_offset(a, series, smp, ti, lam)) : 0.0f;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int q = 0; q < PF_NQ; ++q) {
+          const int smp = lane + 64 * q;
+          if (smp < a.N) {
+            const float trs_s = (float)trend + offs[q * 64 + lane];
+            tv[q] = trs_s;
+            v[q] = fmaf(sd, z[q], fmaf(trs_s, u1, addf));
+          } else {
+            tv[q] = INFINITY;
+            v[q] = INFINITY;
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      }
+      float* buf = s_buf[wave];
+      float a0, a1;
+      wave_select_pair(v, a.k_lo, buf, a0, a1);
+      ylo = np_lerp(a0, a1, a.fr_lo);
+      float nv[PF_NQ];
+#pragma unroll
+      for (int q = 0; q < PF_NQ; ++q) nv[q] = (v[q] == INFINITY) ? INFINITY : -v[q];
+      wave_select_pair(nv, a.k_hi_neg, buf, a0, a1);
+      // a0 = -s[k_hi+1], a1 = -s[k_hi]
+      yhi = np_lerp(-a1, -a0, a.fr_hi);
+      if (future) {
+        wave_select_pair(tv, a.k_lo, buf, a0, a1);
+        tlo = np_lerp(a0, a1, a.fr_lo);
+#pragma unroll
+        for (int q = 0; q < PF_NQ; ++q) nv[q] = (tv[q] == INFINITY) ? INFINITY : -tv[q];
+        wave_select_pair(nv, a.k_hi_neg, buf, a0, a1);
+        thi = np_lerp(-a1, -a0, a.fr_hi);
+      }
+    }
+    if (lane == 0) {
+      const size_t o = (size_t)series * a.Tp + row;
+      a.yhat[o] = (float)yhat;
+      a.ylo[o] = ylo;
+      a.yhi[o] = yhi;
+      if (a.tr) { a.tr[o] = (float)trend; a.trlo[o] = tlo; a.trhi[o] = thi; }
+      if (a.mult) a.mult[o] = (float)xbm;
+      if (a.add) a.add[o] = (float)addt;
+    }
+  }
+}
+
+// ============================================================================
+// C ABI
+// ============================================================================
+extern "C" {
+
+int pf_ctx_create(int device, pf_ctx **out) {
+  if (!out) return set_err(nullptr, "pf_ctx_create: out is NULL");
+  pf_ctx *c = new pf_ctx();
+  c->device = device;
+  c->err[0] = 0;
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) {
+    snprintf(g_err_noctx, sizeof g_err_noctx, "hipSetDevice(%d): %s", device, hipGetErrorString(e));
+    delete c;
+    return -2;
+  }
+  *out = c;
+  return 0;
+}
+
+int pf_ctx_destroy(pf_ctx *ctx) {
+  delete ctx;
+  return 0;
+}
+
+const char *pf_last_error(pf_ctx *ctx) { return ctx ? ctx->err : g_err_noctx; }
+
+void pf_default_fit_opts(pf_fit_opts *o) {
+  o->init_alpha = 1e-3;
+  o->tol_obj = 1e-12;
+  o->tol_rel_obj = 1e4;
+  o->tol_grad = 1e-8;
+  o->tol_rel_grad = 1e7;
+  o->tol_param = 1e-8;
+  o->max_iter = 10000;
+  o->history = 5;
+  o->polish = 1;
+  o->polish_max_iter = 20;
+}
+
+int pf_num_changepoints(int T, int n_changepoints, double changepoint_range) {
+  const int hist_size = (int)floor((double)T * changepoint_range);
+  int n = n_changepoints;
+  if (n + 1 > hist_size) n = hist_size - 1;
+  return n > 0 ? n : 0;
+}
+
+int pf_build_grid(pf_ctx *ctx, const int64_t *ds_ns, int T, int T_pad, int64_t start_ns,
+                  int64_t t_scale_ns, const pf_season *seasons_host, int n_season,
+                  const double *extra_cols, int n_extra, int n_changepoints,
+                  double changepoint_range, double *t_out, double *XT_out, double *t_change_io,
+                  int32_t *cp_idx_out, int32_t *seg_out, int32_t *cp_first_out, int S,
+                  void *stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (T < 1 || T_pad < T || (T_pad % 128) != 0) return set_err(ctx, "pf_build_grid: bad T/T_pad");
+  if (n_season < 0 || n_season > PF_MAX_SEASONS) return set_err(ctx, "pf_build_grid: n_season");
+  if (t_scale_ns <= 0) return set_err(ctx, "pf_build_grid: t_scale must be > 0");
+  if (!ds_ns || !t_out || !XT_out || !t_change_io || !seg_out) return set_err(ctx, "pf_build_grid: NULL buffer");
+  if (S < 1) return set_err(ctx, "pf_build_grid: S must be >= 1");
+  SeasonSpec ss;
+  ss.n = n_season;
+  for (int b = 0; b < n_season; ++b) {
+    ss.period[b] = seasons_host[b].period;
+    ss.order[b] = seasons_host[b].order;
+  }
+  const int nb = (T_pad + 255) / 256;
+  hipLaunchKernelGGL(k_grid_features, dim3(nb), dim3(256), 0, st, ds_ns, T, T_pad, start_ns,
+                     t_scale_ns, ss, extra_cols, n_extra, t_out, XT_out);
+  PF_HIP(ctx, hipGetLastError());
+  if (n_changepoints >= 0) {
+    if (!cp_idx_out) return set_err(ctx, "pf_build_grid: cp_idx_out NULL");
+    const int n_expect = pf_num_changepoints(T, n_changepoints, changepoint_range);
+    if ((n_expect > 0 ? n_expect : 1) != S)
+      return set_err(ctx, "pf_build_grid: S does not match pf_num_changepoints");
+    hipLaunchKernelGGL(k_grid_changepoints, dim3(1), dim3(64), 0, st, t_out, T, n_changepoints,
+                       changepoint_range, t_change_io, cp_idx_out);
+    PF_HIP(ctx, hipGetLastError());
+  }
+  const int ns = ((T_pad > S ? T_pad : S) + 255) / 256;
+  hipLaunchKernelGGL(k_grid_segments, dim3(ns), dim3(256), 0, st, t_out, T, T_pad, t_change_io, S,
+                     seg_out, cp_first_out);
+  PF_HIP(ctx, hipGetLastError());
+  return 0;
+}
+
+int pf_prepare(pf_ctx *ctx, int n_series, const pf_grid *grid, int growth, const double *y,
+               const double *cap, double *y_scale, double *y_scaled, double *cap_scaled,
+               double *theta0, int32_t *status, void *stream) {
+  (void)cap;
+  (void)cap_scaled;
+  if (growth == PF_GROWTH_LOGISTIC) return set_err(ctx, "pf_prepare: logistic growth not supported on the GPU path yet");
+  if (n_series < 0 || !grid || !y || !y_scale || !y_scaled || !theta0 || !status)
+    return set_err(ctx, "pf_prepare: bad arguments");
+  if (n_series == 0) return 0;
+  const int P = 3 + grid->S + grid->K;
+  hipLaunchKernelGGL(k_prepare, dim3(n_series), dim3(256), 0, (hipStream_t)stream, grid->T,
+                     grid->T_pad, grid->t, growth, y, y_scale, y_scaled, theta0, status, P,
+                     grid->S);
+  PF_HIP(ctx, hipGetLastError());
+  return 0;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- dispatch
+namespace {
+
+FitKArgs make_fit_args(const pf_problem *pb) {
+  FitKArgs a;
+  memset(&a, 0, sizeof a);
+  a.T = pb->grid.T;
+  a.Tp = pb->grid.T_pad;
+  a.K = pb->grid.K;
+  a.S = pb->grid.S;
+  a.growth = pb->growth;
+  a.P = 3 + a.S + a.K;
+  a.NB = a.Tp / 64;
+  a.t = pb->grid.t;
+  a.XT = pb->grid.XT;
+  a.t_change = pb->grid.t_change;
+  a.seg = pb->grid.seg;
+  a.sigmas = pb->sigmas;
+  a.s_a = pb->s_a;
+  a.s_m = pb->s_m;
+  a.tau = pb->tau;
+  a.y_scaled = pb->y_scaled;
+  return a;
+}
+
+template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
+int launch_fitlike(pf_ctx *ctx, bool fit, const FitKArgs &a, int n, hipStream_t st) {
+  const size_t smem = FitSmem<NW, KMAX>::bytes(a.Tp, a.NB);
+  if (smem > 160 * 1024) return set_err(ctx, "fit: series too long for the LDS budget");
+  if (fit) {
+    auto kern = k_fit<NW, KMAX, O0, O1, O2, MODE>;
+    PF_HIP(ctx, hipFuncSetAttribute((const void *)kern,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+    hipLaunchKernelGGL(kern, dim3(n), dim3(NW * 64), smem, st, a);
+  } else {
+    auto kern = k_objgrad<NW, KMAX, O0, O1, O2, MODE>;
+    PF_HIP(ctx, hipFuncSetAttribute((const void *)kern,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+    hipLaunchKernelGGL(kern, dim3(n), dim3(NW * 64), smem, st, a);
+  }
+  PF_HIP(ctx, hipGetLastError());
+  return 0;
+}
+
+// Template instances:
+//   (26, 10,3,0, MULT) — the reference's configuration (yearly 10 + weekly 3,
+//                        multiplicative): features regenerated in-register
+//   (26, 10,3,0, ADD/MIXED) — same grid, other seasonality modes
+//   dense fallbacks KMAX 32 / 64 (any K <= KMAX), features read from X^T.
+int dispatch_fitlike(pf_ctx *ctx, bool fit, const FitKArgs &a, int n, int fourier103, int mode,
+                     hipStream_t st) {
+  if (fourier103 && a.K == 26) {
+    if (mode == MODE_MULT) return launch_fitlike<4, 26, 10, 3, 0, MODE_MULT>(ctx, fit, a, n, st);
+    if (mode == MODE_ADD) return launch_fitlike<4, 26, 10, 3, 0, MODE_ADD>(ctx, fit, a, n, st);
+    return launch_fitlike<4, 26, 10, 3, 0, MODE_MIXED>(ctx, fit, a, n, st);
+  }
+  if (a.K <= 32) return launch_fitlike<4, 32, 0, 0, 0, MODE_MIXED>(ctx, fit, a, n, st);
+  if (a.K <= 61) return launch_fitlike<4, 61, 0, 0, 0, MODE_MIXED>(ctx, fit, a, n, st);
+  return set_err(ctx, "fit: K > 61 not supported");
+}
+
+}  // namespace
+
+extern "C" {
+
+static int is_fourier103(const pf_problem *pb) {
+  return pb->fourier_orders[0] == 10 && pb->fourier_orders[1] == 3 && pb->fourier_orders[2] == 0;
+}
+static int mode_of(const pf_problem *pb) {
+  return (pb->season_mode == 0) ? MODE_MULT : (pb->season_mode == 1) ? MODE_ADD : MODE_MIXED;
+}
+
+static int check_problem(pf_ctx *ctx, const pf_problem *pb) {
+  if (!pb) return set_err(ctx, "NULL problem");
+  if (pb->growth == PF_GROWTH_LOGISTIC) return set_err(ctx, "logistic growth not supported on the GPU path yet");
+  const int P = 3 + pb->grid.S + pb->grid.K;
+  if (P > 64) return set_err(ctx, "P = 3 + S + K must be <= 64 on this build");
+  if (pb->grid.S < 1 || pb->grid.S > 62) return set_err(ctx, "S out of range");
+  if (pb->grid.T < 2 || pb->grid.T_pad % 128) return set_err(ctx, "bad T / T_pad");
+  if (!pb->grid.t || !pb->grid.XT || !pb->grid.t_change || !pb->grid.seg || !pb->sigmas ||
+      !pb->s_a || !pb->s_m || !pb->y_scaled)
+    return set_err(ctx, "NULL buffer in problem");
+  return 0;
+}
+
+int pf_objective_grad(pf_ctx *ctx, const pf_problem *pb, const double *theta, double *f,
+                      double *g, void *stream) {
+  int rc = check_problem(ctx, pb);
+  if (rc) return rc;
+  if (pb->n_series == 0) return 0;
+  FitKArgs a = make_fit_args(pb);
+  a.theta = const_cast<double *>(theta);
+  a.f_out = f;
+  a.g_out = g;
+  return dispatch_fitlike(ctx, false, a, pb->n_series, is_fourier103(pb), mode_of(pb),
+                          (hipStream_t)stream);
+}
+
+int pf_fit(pf_ctx *ctx, const pf_problem *pb, const pf_fit_opts *opts, double *theta_inout,
+           double *f_out, double *f_stan, int32_t *status, int32_t *n_iter, int32_t *n_eval,
+           void *stream) {
+  int rc = check_problem(ctx, pb);
+  if (rc) return rc;
+  if (!opts || !theta_inout || !f_out || !f_stan || !status || !n_iter || !n_eval)
+    return set_err(ctx, "pf_fit: NULL output");
+  if (pb->n_series == 0) return 0;
+  FitKArgs a = make_fit_args(pb);
+  a.theta = theta_inout;
+  a.f_out = f_out;
+  a.f_stan = f_stan;
+  a.status = status;
+  a.n_iter = n_iter;
+  a.n_eval = n_eval;
+  a.o = *opts;
+  return dispatch_fitlike(ctx, true, a, pb->n_series, is_fourier103(pb), mode_of(pb),
+                          (hipStream_t)stream);
+}
+
+int pf_predict(pf_ctx *ctx, const pf_predict_args *p, void *stream) {
+  if (!p) return set_err(ctx, "pf_predict: NULL args");
+  if (p->growth == PF_GROWTH_LOGISTIC) return set_err(ctx, "pf_predict: logistic growth not supported on the GPU path yet");
+  if (p->n_samples < 0 || p->n_samples > 64 * PF_NQ) return set_err(ctx, "pf_predict: n_samples must be in [0, 1024]");
+  const int P = 3 + p->fg.S + p->fg.K;
+  if (P > 64 || p->fg.K > 64) return set_err(ctx, "pf_predict: P must be <= 64");
+  if (!p->fg.t || !p->fg.XT || !p->fg.t_change || !p->fg.seg || !p->theta || !p->y_scale ||
+      !p->yhat || !p->yhat_lower || !p->yhat_upper)
+    return set_err(ctx, "pf_predict: NULL buffer");
+  if ((p->trend != nullptr) != (p->trend_lower != nullptr) ||
+      (p->trend != nullptr) != (p->trend_upper != nullptr))
+    return set_err(ctx, "pf_predict: trend/trend_lower/trend_upper must be all set or all NULL");
+  if (p->n_series == 0) return 0;
+  PredKArgs a;
+  memset(&a, 0, sizeof a);
+  a.n_series = p->n_series;
+  a.growth = p->growth;
+  a.N = p->n_samples;
+  a.Tf = p->fg.T;
+  a.Tp = p->fg.T_pad;
+  a.K = p->fg.K;
+  a.S = p->fg.S;
+  a.P = P;
+  a.t = p->fg.t;
+  a.XT = p->fg.XT;
+  a.t_change = p->fg.t_change;
+  a.seg = p->fg.seg;
+  a.s_a = p->s_a;
+  a.s_m = p->s_m;
+  a.theta = p->theta;
+  a.y_scale = p->y_scale;
+  a.seed0 = (uint32_t)(p->seed & 0xFFFFFFFFu);
+  a.seed1 = (uint32_t)(p->seed >> 32);
+  a.yhat = p->yhat;
+  a.ylo = p->yhat_lower;
+  a.yhi = p->yhat_upper;
+  a.tr = p->trend;
+  a.trlo = p->trend_lower;
+  a.trhi = p->trend_upper;
+  a.mult = p->mult_terms;
+  a.add = p->add_terms;
+  if (a.N > 0) {
+    // percentile positions exactly as numpy: q = 100*(1 -/+ w)/2; idx = q/100*(n-1)
+    const double lo_p = 100.0 * (1.0 - p->interval_width) / 2.0;
+    const double hi_p = 100.0 * (1.0 + p->interval_width) / 2.0;
+    const double qlo = lo_p / 100.0, qhi = hi_p / 100.0;
+    const double ilo = a.N * qlo + (1.0 - qlo) - 1.0;  // numpy _compute_virtual_index
+    const double ihi = a.N * qhi + (1.0 - qhi) - 1.0;
+    int klo = (int)floor(ilo), khi = (int)floor(ihi);
+    if (klo > a.N - 2) klo = a.N - 2;
+    if (khi > a.N - 2) khi = a.N - 2;
+    if (klo < 0) klo = 0;
+    if (khi < 0) khi = 0;
+    a.k_lo = klo;
+    a.fr_lo = (float)(ilo - klo);
+    a.k_hi_neg = a.N - 2 - khi;
+    a.fr_hi = (float)(ihi - khi);
+    if (a.N == 1) { a.k_lo = 0; a.fr_lo = 0.f; a.k_hi_neg = 0; a.fr_hi = 0.f; }
+  }
+  const dim3 grid((a.Tf + 15) / 16, a.n_series);
+  hipLaunchKernelGGL((k_predict<64, MODE_MIXED>), grid, dim3(256), 0, (hipStream_t)stream, a);
+  PF_HIP(ctx, hipGetLastError());
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,357 @@
+"""Device-level batched Prophet engine (HIP kernels via the C ABI).
+
+This is the layer the drop-in API (forecaster.py / training.py) and bench.py
+sit on.  Inputs and outputs are torch tensors resident on the GPU; torch is
+only used for device memory and the stream handle.  Every compute step is one
+of the HIP kernels behind include/prophet_hip.h — there is no CPU path.
+
+Mapping to the reference:
+  build_grid      → UPSTREAM setup_dataframe / make_all_seasonality_features /
+                    set_changepoints (02_training.py:172 ``model.fit``)
+  Engine.fit      → PyStan optimizing(LBFGS) on prophet.stan (02_training.py:172)
+  Engine.predict  → make_future_dataframe + predict (02_training.py:201-205,
+                    model_wrapper.py:58-61)
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+NS_PER_DAY = 86400 * 10**9
+
+
+def pad_rows(T: int) -> int:
+    return ((int(T) + 127) // 128) * 128
+
+
+# ---------------------------------------------------------------------------
+# Prophet configuration (the reference's constructor, 02_training.py:162-169)
+# ---------------------------------------------------------------------------
+@dataclass
+class ProphetConfig:
+    growth: str = "linear"
+    n_changepoints: int = 25
+    changepoint_range: float = 0.8
+    yearly_seasonality: object = "auto"
+    weekly_seasonality: object = "auto"
+    daily_seasonality: object = "auto"
+    seasonality_mode: str = "additive"
+    seasonality_prior_scale: float = 10.0
+    holidays_prior_scale: float = 10.0
+    changepoint_prior_scale: float = 0.05
+    interval_width: float = 0.80
+    uncertainty_samples: int = 1000
+
+    @classmethod
+    def reference(cls) -> "ProphetConfig":
+        """Exactly the arguments of notebooks/prophet/02_training.py:162-169."""
+        return cls(interval_width=0.95, growth="linear", daily_seasonality=False,
+                   weekly_seasonality=True, yearly_seasonality=True,
+                   seasonality_mode="multiplicative")
+
+    # UPSTREAM parse_seasonality_args / set_auto_seasonalities
+    @staticmethod
+    def _order(arg, auto_disable, default):
+        if arg == "auto":
+            return 0 if auto_disable else default
+        if arg is True:
+            return default
+        if arg is False or arg is None:
+            return 0
+        return int(arg)
+
+    def seasons(self, first_ns: int, last_ns: int, min_dt_ns: int):
+        span = last_ns - first_ns
+        out = []
+        yo = self._order(self.yearly_seasonality, span < 730 * NS_PER_DAY, 10)
+        if yo > 0:
+            out.append(("yearly", 365.25, yo))
+        wo = self._order(self.weekly_seasonality,
+                         span < 14 * NS_PER_DAY or min_dt_ns >= 7 * NS_PER_DAY, 3)
+        if wo > 0:
+            out.append(("weekly", 7.0, wo))
+        do = self._order(self.daily_seasonality,
+                         span < 2 * NS_PER_DAY or min_dt_ns >= NS_PER_DAY, 4)
+        if do > 0:
+            out.append(("daily", 1.0, do))
+        return out
+
+
+# ---------------------------------------------------------------------------
+# context (one per device)
+# ---------------------------------------------------------------------------
+class Context:
+    _by_device: dict = {}
+
+    def __init__(self, device: int):
+        self.lib = L.load()
+        self.device = device
+        h = ctypes.c_void_p()
+        rc = self.lib.pf_ctx_create(device, ctypes.byref(h))
+        if rc != 0:
+            raise RuntimeError(f"pf_ctx_create failed: {self.lib.pf_last_error(None).decode()}")
+        self.h = h
+
+    @classmethod
+    def get(cls, device: int) -> "Context":
+        if device not in cls._by_device:
+            cls._by_device[device] = Context(device)
+        return cls._by_device[device]
+
+    def check(self, rc: int, what: str):
+        if rc != 0:
+            raise RuntimeError(f"{what} failed ({rc}): {self.lib.pf_last_error(self.h).decode()}")
+
+
+def _stream(device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+# ---------------------------------------------------------------------------
+# K1: device grid
+# ---------------------------------------------------------------------------
+@dataclass
+class DeviceGrid:
+    ds_ns: np.ndarray              # host copy of the grid dates (sorted)
+    start_ns: int
+    t_scale_ns: int
+    seasons: list                  # [(name, period, order)]
+    T: int
+    T_pad: int
+    K: int
+    S: int
+    t: torch.Tensor
+    XT: torch.Tensor
+    t_change: torch.Tensor
+    seg: torch.Tensor
+    cp_first: torch.Tensor
+    cp_idx: torch.Tensor | None = None
+    n_changepoints_placed: int = 0
+
+    def as_pf(self) -> L.PfGrid:
+        return L.PfGrid(self.T, self.T_pad, self.K, self.S, self.t.data_ptr(), self.XT.data_ptr(),
+                        self.t_change.data_ptr(), self.seg.data_ptr(), self.cp_first.data_ptr())
+
+    @property
+    def fourier_orders(self):
+        o = [0, 0, 0]
+        for i, (_, _, order) in enumerate(self.seasons[:3]):
+            o[i] = order
+        return o
+
+
+def build_grid(ds_ns: np.ndarray, seasons, *, start_ns: int, t_scale_ns: int,
+               n_changepoints: int = 25, changepoint_range: float = 0.8,
+               t_change: torch.Tensor | None = None, device: int = 0) -> DeviceGrid:
+    """Design grid on the GPU (K1).  With ``t_change=None`` the changepoints are
+    placed (fit grid); otherwise they are reused (predict grid)."""
+    ctx = Context.get(device)
+    ds_ns = np.ascontiguousarray(np.asarray(ds_ns, dtype=np.int64))
+    T = int(ds_ns.shape[0])
+    Tp = pad_rows(T)
+    K = sum(2 * o for _, _, o in seasons)
+    if K == 0:
+        raise ValueError("no seasonality columns: the zero-feature dummy X is not supported yet")
+    dev = torch.device("cuda", device)
+    ds_d = torch.from_numpy(ds_ns).to(dev)
+    t = torch.empty(Tp, dtype=torch.float64, device=dev)
+    XT = torch.empty(K * Tp, dtype=torch.float64, device=dev)
+    seg = torch.empty(Tp, dtype=torch.int32, device=dev)
+    sp = (L.PfSeason * max(1, len(seasons)))()
+    for i, (_, period, order) in enumerate(seasons):
+        sp[i].period = float(period)
+        sp[i].order = int(order)
+    if t_change is None:
+        S_eff = L.num_changepoints(T, n_changepoints, changepoint_range)
+        S = max(S_eff, 1)
+        tc = torch.empty(S, dtype=torch.float64, device=dev)
+        cp_idx = torch.empty(S, dtype=torch.int32, device=dev)
+        ncp = n_changepoints
+    else:
+        tc = t_change
+        S = int(tc.numel())
+        cp_idx = None
+        ncp = -1
+        S_eff = S
+    cp_first = torch.empty(S, dtype=torch.int32, device=dev)
+    rc = ctx.lib.pf_build_grid(ctx.h, _ptr(ds_d), T, Tp, int(start_ns), int(t_scale_ns), sp,
+                               len(seasons), None, 0, ncp, float(changepoint_range), _ptr(t),
+                               _ptr(XT), _ptr(tc), _ptr(cp_idx), _ptr(seg), _ptr(cp_first), S,
+                               _stream(device))
+    ctx.check(rc, "pf_build_grid")
+    return DeviceGrid(ds_ns, int(start_ns), int(t_scale_ns), list(seasons), T, Tp, K, S, t, XT,
+                      tc, seg, cp_first, cp_idx, S_eff)
+
+
+def future_dates(history_dates_ns: np.ndarray, periods: int, freq_ns: int = NS_PER_DAY,
+                 include_history: bool = True) -> np.ndarray:
+    """UPSTREAM make_future_dataframe: unique history dates + ``periods`` more."""
+    h = np.unique(np.asarray(history_dates_ns, np.int64))
+    last = int(h[-1])
+    fut = last + freq_ns * np.arange(1, periods + 1, dtype=np.int64)
+    return np.concatenate((h, fut)) if include_history else fut
+
+
+# ---------------------------------------------------------------------------
+# K2/K3 fit, K4/K5 predict
+# ---------------------------------------------------------------------------
+@dataclass
+class FitResult:
+    grid: DeviceGrid
+    theta: torch.Tensor      # [n, P] float64
+    y_scale: torch.Tensor    # [n]
+    f: torch.Tensor          # [n] -log posterior at the returned theta
+    f_stan: torch.Tensor     # [n] where the Stan-faithful phase stopped
+    status: torch.Tensor     # [n] int32
+    n_iter: torch.Tensor
+    n_eval: torch.Tensor
+    config: ProphetConfig = field(default_factory=ProphetConfig)
+
+    @property
+    def P(self):
+        return self.theta.shape[1]
+
+
+class Engine:
+    """Batched Prophet engine bound to one GPU."""
+
+    def __init__(self, device: int = 0, config: ProphetConfig | None = None):
+        self.device = device
+        self.ctx = Context.get(device)
+        self.config = config or ProphetConfig.reference()
+        self._vec_cache = {}
+
+    # prior scales and mode indicators (UPSTREAM regressor_column_matrix)
+    def _vectors(self, grid: DeviceGrid):
+        key = (grid.K, tuple(grid.seasons), self.config.seasonality_mode,
+               self.config.seasonality_prior_scale)
+        if key not in self._vec_cache:
+            dev = torch.device("cuda", self.device)
+            mult = self.config.seasonality_mode == "multiplicative"
+            sig = torch.full((grid.K,), float(self.config.seasonality_prior_scale),
+                             dtype=torch.float64, device=dev)
+            s_m = torch.full((grid.K,), 1.0 if mult else 0.0, dtype=torch.float64, device=dev)
+            s_a = torch.full((grid.K,), 0.0 if mult else 1.0, dtype=torch.float64, device=dev)
+            self._vec_cache[key] = (sig, s_a, s_m, 0 if mult else 1)
+        return self._vec_cache[key]
+
+    def problem(self, grid: DeviceGrid, y_scaled: torch.Tensor, n: int) -> L.PfProblem:
+        sig, s_a, s_m, mode = self._vectors(grid)
+        pb = L.PfProblem()
+        pb.n_series = n
+        pb.growth = L.PF_GROWTH[self.config.growth]
+        pb.tau = float(self.config.changepoint_prior_scale)
+        pb.grid = grid.as_pf()
+        pb.sigmas, pb.s_a, pb.s_m = sig.data_ptr(), s_a.data_ptr(), s_m.data_ptr()
+        pb.y_scaled = y_scaled.data_ptr()
+        pb.cap_scaled = None
+        fo = grid.fourier_orders
+        for i in range(3):
+            pb.fourier_orders[i] = fo[i]
+        pb.season_mode = mode
+        pb._keep = (sig, s_a, s_m, y_scaled)
+        return pb
+
+    def prepare(self, grid: DeviceGrid, Y: torch.Tensor):
+        """y_scale, y_scaled and Prophet's init theta0 on the device."""
+        n = Y.shape[0]
+        assert Y.dtype == torch.float64 and Y.shape[1] == grid.T_pad and Y.is_contiguous()
+        dev = Y.device
+        P = 3 + grid.S + grid.K
+        y_scale = torch.empty(n, dtype=torch.float64, device=dev)
+        y_scaled = torch.empty_like(Y)
+        theta = torch.empty((n, P), dtype=torch.float64, device=dev)
+        status = torch.empty(n, dtype=torch.int32, device=dev)
+        pg = grid.as_pf()
+        rc = self.ctx.lib.pf_prepare(self.ctx.h, n, ctypes.byref(pg),
+                                     L.PF_GROWTH[self.config.growth], _ptr(Y), None,
+                                     _ptr(y_scale), _ptr(y_scaled), None, _ptr(theta),
+                                     _ptr(status), _stream(self.device))
+        self.ctx.check(rc, "pf_prepare")
+        return y_scale, y_scaled, theta, status
+
+    def objective_grad(self, grid: DeviceGrid, y_scaled: torch.Tensor, theta: torch.Tensor):
+        n = theta.shape[0]
+        f = torch.empty(n, dtype=torch.float64, device=theta.device)
+        g = torch.empty_like(theta)
+        pb = self.problem(grid, y_scaled, n)
+        rc = self.ctx.lib.pf_objective_grad(self.ctx.h, ctypes.byref(pb), _ptr(theta), _ptr(f),
+                                            _ptr(g), _stream(self.device))
+        self.ctx.check(rc, "pf_objective_grad")
+        return f, g
+
+    def fit_opts(self, polish: bool = True, **over) -> L.PfFitOpts:
+        o = L.PfFitOpts()
+        self.ctx.lib.pf_default_fit_opts(ctypes.byref(o))
+        o.polish = 1 if polish else 0
+        for k, v in over.items():
+            setattr(o, k, v)
+        return o
+
+    def fit(self, grid: DeviceGrid, Y: torch.Tensor, polish: bool = True, **opt) -> FitResult:
+        """Fit every row of Y [n, T_pad] (raw y, float64, on this GPU)."""
+        n = Y.shape[0]
+        y_scale, y_scaled, theta, status = self.prepare(grid, Y)
+        dev = Y.device
+        f = torch.empty(n, dtype=torch.float64, device=dev)
+        f_stan = torch.empty(n, dtype=torch.float64, device=dev)
+        n_iter = torch.empty(n, dtype=torch.int32, device=dev)
+        n_eval = torch.empty(n, dtype=torch.int32, device=dev)
+        pb = self.problem(grid, y_scaled, n)
+        o = self.fit_opts(polish, **opt)
+        rc = self.ctx.lib.pf_fit(self.ctx.h, ctypes.byref(pb), ctypes.byref(o), _ptr(theta),
+                                 _ptr(f), _ptr(f_stan), _ptr(status), _ptr(n_iter), _ptr(n_eval),
+                                 _stream(self.device))
+        self.ctx.check(rc, "pf_fit")
+        return FitResult(grid, theta, y_scale, f, f_stan, status, n_iter, n_eval, self.config)
+
+    def predict_grid(self, fit: FitResult, ds_ns: np.ndarray) -> DeviceGrid:
+        g = fit.grid
+        return build_grid(ds_ns, g.seasons, start_ns=g.start_ns, t_scale_ns=g.t_scale_ns,
+                          changepoint_range=self.config.changepoint_range, t_change=g.t_change,
+                          device=self.device)
+
+    def predict(self, fit: FitResult, fgrid: DeviceGrid, n_samples: int | None = None,
+                seed: int = 0, components: bool = True) -> dict:
+        """Point forecast + MC intervals for every fitted series on ``fgrid``.
+        Returns float32 device tensors [n, fgrid.T_pad] (valid columns :T)."""
+        n = fit.theta.shape[0]
+        dev = fit.theta.device
+        ns = self.config.uncertainty_samples if n_samples is None else n_samples
+        sig, s_a, s_m, _ = self._vectors(fgrid)
+        out = {k: torch.empty((n, fgrid.T_pad), dtype=torch.float32, device=dev)
+               for k in ("yhat", "yhat_lower", "yhat_upper")}
+        if components:
+            for k in ("trend", "trend_lower", "trend_upper", "multiplicative_terms",
+                      "additive_terms"):
+                out[k] = torch.empty((n, fgrid.T_pad), dtype=torch.float32, device=dev)
+        a = L.PfPredictArgs()
+        a.n_series = n
+        a.growth = L.PF_GROWTH[self.config.growth]
+        a.n_samples = int(ns)
+        a.fg = fgrid.as_pf()
+        a.s_a, a.s_m = s_a.data_ptr(), s_m.data_ptr()
+        a.theta = fit.theta.data_ptr()
+        a.y_scale = fit.y_scale.data_ptr()
+        a.cap_scaled = None
+        a.interval_width = float(self.config.interval_width)
+        a.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        a.yhat, a.yhat_lower, a.yhat_upper = (out[k].data_ptr() for k in
+                                              ("yhat", "yhat_lower", "yhat_upper"))
+        if components:
+            a.trend, a.trend_lower, a.trend_upper = (out[k].data_ptr() for k in
+                                                     ("trend", "trend_lower", "trend_upper"))
+            a.mult_terms = out["multiplicative_terms"].data_ptr()
+            a.add_terms = out["additive_terms"].data_ptr()
+        rc = self.ctx.lib.pf_predict(self.ctx.h, ctypes.byref(a), _stream(self.device))
+        self.ctx.check(rc, "pf_predict")
+        return out

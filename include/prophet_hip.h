@@ -1,0 +1,167 @@
+/*
+ * prophet_hip.h — C ABI of the MI355X (gfx950) batched Prophet engine.
+ *
+ * This is the drop-in boundary for the reference's per-group hot path
+ * (SURVEY.md §8b).  The reference binds Prophet through Python only:
+ *   - fit:      Prophet(...).fit(history_pd)           notebooks/prophet/02_training.py:162-172
+ *               (→ PyStan optimizing(LBFGS), UPSTREAM)
+ *   - forecast: make_future_dataframe(90,'d') + predict  notebooks/prophet/02_training.py:201-205
+ *               and model.predict(future_df)             notebooks/prophet/model_wrapper.py:58-61
+ * Each entry point below replaces one of those upstream calls for a whole
+ * batch of series at once.  The Python host layer (distributed-forecasting_amd/)
+ * binds them with ctypes exactly as INTEGRATION.md shows.
+ *
+ * Conventions
+ *   - Every buffer is a caller-owned DEVICE pointer (e.g. torch tensor
+ *     data_ptr()).  The library never frees caller memory; scratch lives in
+ *     the opaque context.
+ *   - Every call is asynchronous on the caller's hipStream_t (passed as void*).
+ *   - Return value: 0 = ok, <0 = argument / HIP error (pf_last_error() has
+ *     the message).  Per-series outcomes are reported in status arrays, never
+ *     as a non-zero return.
+ *   - A context is per device and must not be shared between host threads.
+ *
+ * Parameter vector per series (Stan unconstrained order, fp64):
+ *   theta = [k, m, delta[S], log(sigma_obs), beta[K]],  P = 3 + S + K.
+ */
+#ifndef PROPHET_HIP_H
+#define PROPHET_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct pf_ctx pf_ctx;
+
+enum pf_growth { PF_GROWTH_LINEAR = 0, PF_GROWTH_LOGISTIC = 1, PF_GROWTH_FLAT = 2 };
+
+/* Per-series fit status (Stan bfgs.hpp TERM_* codes + engine extras). */
+enum pf_status {
+  PF_ST_SUCCESS = 0, PF_ST_ABSX = 10, PF_ST_ABSF = 20, PF_ST_RELF = 21,
+  PF_ST_ABSGRAD = 30, PF_ST_RELGRAD = 31, PF_ST_MAXIT = 40,
+  PF_ST_LSFAIL = -1, PF_ST_BADINIT = -2,
+  PF_ST_CONSTANT = 50          /* min y == max y: optimizer skipped (Prophet rule) */
+};
+
+/* One Fourier seasonality block: columns sin/cos(2π(i+1)d/period), i<order. */
+typedef struct { double period; int32_t order; int32_t _pad; } pf_season;
+
+/* A shared date grid (all series of a batch share their non-NaN dates).
+ * Rows are padded to T_pad = round_up(T, 128); buffers use stride T_pad. */
+typedef struct {
+  int32_t T;            /* valid rows                                       */
+  int32_t T_pad;        /* row stride of XT / y buffers (multiple of 128)   */
+  int32_t K;            /* feature columns                                  */
+  int32_t S;            /* changepoints (>= 1; dummy t_change=[0] if none)  */
+  const double *t;      /* [T_pad]   (ds - start)/t_scale                   */
+  const double *XT;     /* [K*T_pad] features, feature-major                */
+  const double *t_change;  /* [S]                                           */
+  const int32_t *seg;   /* [T_pad]   #{j : t_change[j] <= t[i]}             */
+  const int32_t *cp_first; /* [S]    first row with t >= t_change[j]         */
+} pf_grid;
+
+/* The Stan data block for a batch of n_series series on one grid. */
+typedef struct {
+  int32_t n_series;
+  int32_t growth;       /* pf_growth */
+  double tau;           /* changepoint_prior_scale                          */
+  pf_grid grid;
+  const double *sigmas; /* [K] prior scales                                 */
+  const double *s_a;    /* [K] additive indicator                           */
+  const double *s_m;    /* [K] multiplicative indicator                     */
+  const double *y_scaled; /* [n_series*T_pad] y / y_scale (pad rows ignored) */
+  const double *cap_scaled; /* [n_series*T_pad] or NULL (logistic only)     */
+  /* Layout hints (host-known, avoid device reads):
+   *   fourier_orders: orders of the Fourier blocks occupying the first
+   *     2*sum(orders) columns of X (e.g. {10,3,0} = yearly+weekly); lets the
+   *     kernel regenerate harmonics in-register. {0,0,0} = read X densely.
+   *   season_mode: 0 = every column multiplicative (s_m=1,s_a=0),
+   *                1 = every column additive, 2 = mixed.                   */
+  int32_t fourier_orders[3];
+  int32_t season_mode;
+} pf_problem;
+
+typedef struct {
+  /* Stan optimizing() defaults as PyStan 2.19 / Prophet pass them */
+  double init_alpha, tol_obj, tol_rel_obj, tol_grad, tol_rel_grad, tol_param;
+  int32_t max_iter, history;
+  /* engine: exact-MAP proximal-Newton polish after the Stan phase (0/1) */
+  int32_t polish, polish_max_iter;
+} pf_fit_opts;
+
+/* ---------------------------------------------------------------- context */
+int pf_ctx_create(int device, pf_ctx **out);
+int pf_ctx_destroy(pf_ctx *ctx);
+const char *pf_last_error(pf_ctx *ctx);
+void pf_default_fit_opts(pf_fit_opts *o);
+
+/* Host-side helper (no GPU): number of changepoints Prophet will place for a
+ * history of T rows (set_changepoints clamp: n_cp+1 > floor(T*range) → floor-1). */
+int pf_num_changepoints(int T, int n_changepoints, double changepoint_range);
+
+/* ----------------------------------------------------- K1: design builder
+ * Replaces UPSTREAM setup_dataframe (t), make_all_seasonality_features (X)
+ * and set_changepoints + Stan get_changepoint_matrix (t_change, segments).
+ *   ds_ns [T] sorted int64 ns; start_ns / t_scale_ns from the fit history.
+ *   extra_cols [n_extra*T] (holidays / regressors, feature-major) or NULL.
+ *   n_changepoints < 0  → do not place changepoints (predict grids reuse the
+ *   fit's t_change and only get seg[]).                                     */
+int pf_build_grid(pf_ctx *ctx, const int64_t *ds_ns, int T, int T_pad,
+                  int64_t start_ns, int64_t t_scale_ns,
+                  const pf_season *seasons_host, int n_season,
+                  const double *extra_cols, int n_extra,
+                  int n_changepoints, double changepoint_range,
+                  double *t_out, double *XT_out,
+                  double *t_change_io, int32_t *cp_idx_out,
+                  int32_t *seg_out, int32_t *cp_first_out, int S,
+                  void *stream);
+
+/* ------------------------------------------ scaling + Prophet init (a1, a4)
+ * y [n_series*T_pad] raw (pad rows ignored) → y_scale[n], y_scaled[n*T_pad],
+ * theta0[n*P] (linear_growth_init; delta=beta=0; sigma_obs=1) and
+ * status[n] = PF_ST_CONSTANT where min y == max y (else 0).               */
+int pf_prepare(pf_ctx *ctx, int n_series, const pf_grid *grid, int growth,
+               const double *y, const double *cap,
+               double *y_scale, double *y_scaled, double *cap_scaled,
+               double *theta0, int32_t *status, void *stream);
+
+/* ------------------------------------------- K2: batched objective + grad
+ * f[n] = -log posterior (Stan propto), g[n*P] = its gradient.            */
+int pf_objective_grad(pf_ctx *ctx, const pf_problem *pb, const double *theta,
+                      double *f, double *g, void *stream);
+
+/* -------------------------------------------------- K3: batched fit (MAP)
+ * theta_inout[n*P]: init in, optimum out.  f_out[n] final -log posterior,
+ * f_stan[n] objective where the Stan-faithful phase stopped, status[n]
+ * (in: PF_ST_CONSTANT rows are skipped), n_iter[n], n_eval[n].           */
+int pf_fit(pf_ctx *ctx, const pf_problem *pb, const pf_fit_opts *opts,
+           double *theta_inout, double *f_out, double *f_stan,
+           int32_t *status, int32_t *n_iter, int32_t *n_eval, void *stream);
+
+/* ------------------------------ K4+K5: forecast + Monte-Carlo intervals
+ * Future grid fg (t relative to the fit's start/t_scale; seg vs the fit's
+ * t_change).  Outputs fp32 [n*fg.T_pad] (stride T_pad).  n_samples <= 1024;
+ * n_samples == 0 skips the intervals (lower/upper = point).  trend_* and
+ * the component outputs may be NULL.                                     */
+typedef struct {
+  int32_t n_series, growth, n_samples, _pad;
+  pf_grid fg;
+  const double *s_a, *s_m;
+  const double *theta;        /* [n*P] */
+  const double *y_scale;      /* [n]   */
+  const double *cap_scaled;   /* [n*fg.T_pad] or NULL */
+  double interval_width;
+  uint64_t seed;
+  float *yhat, *yhat_lower, *yhat_upper;
+  float *trend, *trend_lower, *trend_upper;
+  float *mult_terms, *add_terms;
+} pf_predict_args;
+
+int pf_predict(pf_ctx *ctx, const pf_predict_args *args, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PROPHET_HIP_H */
