@@ -126,6 +126,50 @@ __device__ __forceinline__ double wave_suffix_sum(double v, double &tot) {
   return tot - p + v;
 }
 
+// Sum N <= 32 independent per-lane values over the wave by recursive halving
+// (32 shuffle+add pairs instead of 6*N); out[v] is the uniform total of v.
+template <int N>
+__device__ __forceinline__ void wave_sum_multi(const double (&v)[N], double (&out)[N]) {
+  static_assert(N <= 32, "wave_sum_multi: N <= 32");
+  const int lane = pf_lane();
+  double w16[16], w8[8], w4[4], w2[2], w1;
+  // level xor 32: value pair (2k, 2k+1) -> lanes <32 keep 2k, >=32 keep 2k+1
+  const bool h5 = lane & 32, h4 = lane & 16, h3 = lane & 8, h2 = lane & 4, h1 = lane & 2;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const double a = (2 * k < N) ? v[2 * k] : 0.0, b = (2 * k + 1 < N) ? v[2 * k + 1] : 0.0;
+    const double keep = h5 ? b : a, send = h5 ? a : b;
+    w16[k] = keep + shfl_xor_f64<32>(send);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const double keep = h4 ? w16[2 * k + 1] : w16[2 * k], send = h4 ? w16[2 * k] : w16[2 * k + 1];
+    w8[k] = keep + shfl_xor_f64<16>(send);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const double keep = h3 ? w8[2 * k + 1] : w8[2 * k], send = h3 ? w8[2 * k] : w8[2 * k + 1];
+    w4[k] = keep + shfl_xor_f64<8>(send);
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const double keep = h2 ? w4[2 * k + 1] : w4[2 * k], send = h2 ? w4[2 * k] : w4[2 * k + 1];
+    w2[k] = keep + shfl_xor_f64<4>(send);
+  }
+  {
+    const double keep = h1 ? w2[1] : w2[0], send = h1 ? w2[0] : w2[1];
+    w1 = keep + shfl_xor_f64<2>(send);
+  }
+  w1 += shfl_xor_f64<1>(w1);
+  // value index held by lane l: bit0 <- lane bit5, bit1 <- bit4, ... bit4 <- bit1
+#pragma unroll
+  for (int idx = 0; idx < N; ++idx) {
+    const int l = ((idx & 1) << 5) | (((idx >> 1) & 1) << 4) | (((idx >> 2) & 1) << 3) |
+                  (((idx >> 3) & 1) << 2) | (((idx >> 4) & 1) << 1);
+    out[idx] = readlane_f64(w1, l);
+  }
+}
+
 // ---------------------------------------------------------------- Philox4x32-10
 struct pf_u4 { uint32_t x, y, z, w; };
 

@@ -28,9 +28,24 @@
 struct pf_ctx {
   int device;
   char err[512];
+  void *ws;         // scratch owned by the context (polish per-row scalars)
+  size_t ws_bytes;
 };
 
 static char g_err_noctx[512] = "";
+
+// Diagnostic build only (-DPF_STAMPS, tools/stamps.py): s_memtime sums at
+// phase boundaries of block 0 / thread 0.  Never compiled into the product.
+#ifdef PF_STAMPS
+__device__ unsigned long long pf_dbg[32];
+#define PF_STAMP(i)                                                              \
+  do {                                                                           \
+    if (blockIdx.x == 0 && threadIdx.x == 0)                                     \
+      atomicAdd(&pf_dbg[i], (unsigned long long)__builtin_amdgcn_s_memtime());   \
+  } while (0)
+#else
+#define PF_STAMP(i) do { } while (0)
+#endif
 
 static int set_err(pf_ctx *ctx, const char *msg) {
   char *dst = ctx ? ctx->err : g_err_noctx;
@@ -222,6 +237,7 @@ struct FitKArgs {
   const double *sigmas, *s_a, *s_m;
   double tau;
   const double *y_scaled;
+  double *ws;  // polish workspace [n][3][Tp]
   // fit
   double *theta;
   double *f_out, *f_stan, *g_out;
@@ -314,10 +330,14 @@ __device__ __forceinline__ void row_features(const double *__restrict__ XT, int 
   for (int f = KF; f < KMAX; ++f) x[f] = (f < K) ? XT[(size_t)f * Tp + i] : 0.0;
 }
 
-static constexpr size_t kLbBytes = 12 * 1024;
+static constexpr size_t kLbBytes = 9 * 1024;
 struct LbLds;
-template <int NW, int KMAX>
+// LDS layout of the fit kernel.  Fixed part + a union region U that holds
+// {beta-gradient partials, L-BFGS state} during the Stan phase and
+// {Hessian tile reduction, H, Cholesky workspace} during the polish.
+template <int NW, int KMAX, int MODE = 2>
 struct FitSmem {
+  static constexpr int NSET = 2;  // (mult, add) partial-set slots (index by set)
   double *y;        // [Tp]
   double *th;       // [64]
   double *kseg;     // [64]
@@ -325,19 +345,34 @@ struct FitSmem {
   double *bm, *ba;  // [KMAX]
   double *bsum0, *bsum1;  // [NB]
   double *cps0, *cps1;    // [64]
-  int *cpb;               // [64]
-  double *gbt;      // [NW][2][KMAX][64]
   double *rrw;      // [NW]
   double *gout;     // [64]
-  double *fout;     // [4]: f, bad
+  double *fout;     // [4]
   double *gb;       // [2][KMAX] reduced
-  struct LbLds *lb;
-  static __host__ __device__ size_t bytes(int Tp, int NB) {
-    return sizeof(double) * ((size_t)Tp + 64 * 3 + 2 * KMAX + 2 * (size_t)NB + 128 +
-                             (size_t)NW * 2 * KMAX * 64 + NW + 64 + 4 + 2 * KMAX) +
-           sizeof(int) * 64 + 64 + kLbBytes;
+  double *pd, *pz;  // [64] polish direction / scratch
+  int *cpb;         // [64]
+  int *qmap;        // [64]
+  double *U;        // union region
+  double *gbt;      // U view: [NW][NSET][KMAX][32]
+  struct LbLds *lb; // U view, after gbt
+  int LD;           // stride of H / M in U (polish)
+  static __host__ __device__ size_t fixed_doubles(int Tp, int NB) {
+    return (size_t)Tp + 64 * 3 + 2 * KMAX + 2 * (size_t)NB + 128 + NW + 64 + 4 + 2 * KMAX + 128 + 64;
   }
-  __device__ void carve(char *base, int Tp, int NB) {
+  // MULT / ADD use one partial set, MIXED two
+  static __host__ __device__ size_t gbt_doubles() { return (size_t)NW * (MODE == 2 ? 2 : 1) * KMAX * 32; }
+  static __host__ __device__ size_t union_bytes(int P) {
+    const size_t eval = gbt_doubles() * sizeof(double) + kLbBytes;
+    const size_t tiles = (size_t)10 * 4 * 64 * sizeof(double);
+    const int LD = P | 1;
+    const size_t hm = 2 * (size_t)P * LD * sizeof(double);
+    size_t u = eval > tiles ? eval : tiles;
+    return u > hm ? u : hm;
+  }
+  static __host__ __device__ size_t bytes(int Tp, int NB, int P) {
+    return fixed_doubles(Tp, NB) * sizeof(double) + union_bytes(P) + 64;
+  }
+  __device__ void carve(char *base, int Tp, int NB, int P) {
     double *p = reinterpret_cast<double *>(base);
     y = p; p += Tp;
     th = p; p += 64;
@@ -349,54 +384,66 @@ struct FitSmem {
     bsum1 = p; p += NB;
     cps0 = p; p += 64;
     cps1 = p; p += 64;
-    gbt = p; p += (size_t)NW * 2 * KMAX * 64;
     rrw = p; p += NW;
     gout = p; p += 64;
     fout = p; p += 4;
     gb = p; p += 2 * KMAX;
-    cpb = reinterpret_cast<int *>(p);
-    // align via offsets from the LDS base (an integer round trip would lose
-    // the address space and turn every access into a flat op)
-    size_t off = (size_t)(reinterpret_cast<char *>(cpb + 64) - base);
+    pd = p; p += 64;
+    pz = p; p += 64;
+    cpb = reinterpret_cast<int *>(p); p += 32;
+    qmap = reinterpret_cast<int *>(p); p += 32;
+    // 16-byte align U via offsets from the LDS base (keeps the address space)
+    size_t off = (size_t)(reinterpret_cast<char *>(p) - base);
     off = (off + 15) & ~(size_t)15;
-    lb = reinterpret_cast<struct LbLds *>(base + off);
+    U = reinterpret_cast<double *>(base + off);
+    gbt = U;
+    lb = reinterpret_cast<struct LbLds *>(reinterpret_cast<char *>(U) + gbt_doubles() * sizeof(double));
+    LD = P | 1;
   }
 };
+
+template <int NW, int KMAX, int MODE>
+__device__ __forceinline__ void publish_theta(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, double x) {
+  const int lane = pf_lane();
+  if (pf_wave() != 0) return;
+  const int P = a.P, S = a.S, K = a.K;
+  if (lane < P) sm.th[lane] = x;
+  const double k = readlane_f64(x, 0), m = readlane_f64(x, 1);
+  // delta_j sits in lane 2+j
+  const double dj = __shfl(x, (lane + 2) & 63, 64);
+  const double dval = (lane < S) ? dj : 0.0;
+  const double tcd = (lane < S) ? a.t_change[lane] * dval : 0.0;
+  const double cd = wave_prefix_sum(dval);   // inclusive: sum_{j<=lane}
+  const double ctd = wave_prefix_sum(tcd);
+  // kseg[s] = k + sum_{j<s} delta_j ; mseg[s] = m - sum_{j<s} tc_j delta_j
+  const double cd_ex = wave_shift_up1(cd);
+  const double ctd_ex = wave_shift_up1(ctd);
+  if (lane <= S) {
+    sm.kseg[lane] = k + (lane == 0 ? 0.0 : cd_ex);
+    sm.mseg[lane] = m - (lane == 0 ? 0.0 : ctd_ex);
+  }
+  const double bval = __shfl(x, (lane + 3 + S) & 63, 64);
+  if (lane < KMAX) {
+    const double bv = (lane < K) ? bval : 0.0;
+    sm.bm[lane] = bv * ((lane < K) ? a.s_m[lane] : 0.0);
+    sm.ba[lane] = bv * ((lane < K) ? a.s_a[lane] : 0.0);
+  }
+}
 
 // One collective evaluation of f(theta) = -log posterior and its gradient.
 // Every thread of the workgroup must call it.  `x` is this lane's parameter
 // (lane p < P); returns f in every thread and g (lane p) in `g`; returns true
 // if f or g is not finite (Stan ModelAdaptor error → line-search retreat).
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
-__device__ bool eval_collective(const FitKArgs &a, FitSmem<NW, KMAX> &sm, double x, double &f,
+__device__ bool eval_collective(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, double x, double &f,
                                 double &g) {
   const int lane = pf_lane(), wave = pf_wave();
   const int P = a.P, S = a.S, K = a.K, T = a.T, Tp = a.Tp;
   // ---- phase 0: wave 0 publishes theta and the segment rates/offsets
-  if (wave == 0) {
-    if (lane < P) sm.th[lane] = x;
-    const double k = readlane_f64(x, 0), m = readlane_f64(x, 1);
-    // delta_j sits in lane 2+j
-    const double dj = __shfl(x, (lane + 2) & 63, 64);
-    const double dval = (lane < S) ? dj : 0.0;
-    const double tcd = (lane < S) ? a.t_change[lane] * dval : 0.0;
-    const double cd = wave_prefix_sum(dval);   // inclusive: sum_{j<=lane}
-    const double ctd = wave_prefix_sum(tcd);
-    // kseg[s] = k + sum_{j<s} delta_j ; mseg[s] = m - sum_{j<s} tc_j delta_j
-    const double cd_ex = wave_shift_up1(cd);
-    const double ctd_ex = wave_shift_up1(ctd);
-    if (lane <= S) {
-      sm.kseg[lane] = k + (lane == 0 ? 0.0 : cd_ex);
-      sm.mseg[lane] = m - (lane == 0 ? 0.0 : ctd_ex);
-    }
-    const double bval = __shfl(x, (lane + 3 + S) & 63, 64);
-    if (lane < KMAX) {
-      const double bv = (lane < K) ? bval : 0.0;
-      sm.bm[lane] = bv * ((lane < K) ? a.s_m[lane] : 0.0);
-      sm.ba[lane] = bv * ((lane < K) ? a.s_a[lane] : 0.0);
-    }
-  }
+  PF_STAMP(0);
+  publish_theta<NW, KMAX, MODE>(a, sm, x);
   __syncthreads();
+  PF_STAMP(1);
   // ---- phase 1: row pass (batch of 64 consecutive rows per wave iteration)
   double gbm[KMAX], gba[KMAX];
 #pragma unroll
@@ -404,8 +451,13 @@ __device__ bool eval_collective(const FitKArgs &a, FitSmem<NW, KMAX> &sm, double
     gbm[f2] = 0.0;
     gba[f2] = 0.0;
   }
-  const double *lbm = sm.bm;
-  const double *lba = sm.ba;
+  // beta coefficients in registers for the whole pass (uniform values)
+  double lbm[KMAX], lba[KMAX];
+#pragma unroll
+  for (int f2 = 0; f2 < KMAX; ++f2) {
+    lbm[f2] = (MODE != MODE_ADD) ? sm.bm[f2] : 0.0;
+    lba[f2] = (MODE != MODE_MULT) ? sm.ba[f2] : 0.0;
+  }
   const double th_m = sm.th[1];
   const bool linear = (a.growth == PF_GROWTH_LINEAR);
   double rr = 0.0;
@@ -426,9 +478,6 @@ __device__ bool eval_collective(const FitKArgs &a, FitSmem<NW, KMAX> &sm, double
     for (int f2 = 0; f2 < KMAX; ++f2) {
       if constexpr (MODE != MODE_ADD) xm[f2 & 3] = fma(xf[f2], lbm[f2], xm[f2 & 3]);
       if constexpr (MODE != MODE_MULT) xa[f2 & 3] = fma(xf[f2], lba[f2], xa[f2 & 3]);
-      // stream the (uniform) coefficient loads in groups of 8 instead of
-      // letting the scheduler hoist all KMAX of them (register pressure)
-      if ((f2 & 7) == 7) __builtin_amdgcn_sched_barrier(0);
     }
     const double xbm = (xm[0] + xm[1]) + (xm[2] + xm[3]);
     const double xba = (xa[0] + xa[1]) + (xa[2] + xa[3]);
@@ -461,20 +510,29 @@ __device__ bool eval_collective(const FitKArgs &a, FitSmem<NW, KMAX> &sm, double
     }
     cur = nxt;
   }
+  PF_STAMP(2);
   // ---- phase 2: transpose-reduce the beta gradient partials through LDS
+  // (one permlane32 step first: 32 partials per feature per wave)
   rr = wave_sum(rr);
   if (lane == 0) sm.rrw[wave] = rr;
   {
-    double *gw = sm.gbt + (size_t)wave * 2 * KMAX * 64;
+    constexpr int NS = (MODE == MODE_MIXED) ? 2 : 1;
+    double *gw = sm.gbt + (size_t)wave * NS * KMAX * 32;
 #pragma unroll
     for (int f2 = 0; f2 < KMAX; ++f2) {
-      if constexpr (MODE != MODE_ADD) gw[f2 * 64 + lane] = gbm[f2];
-      if constexpr (MODE != MODE_MULT) gw[(KMAX + f2) * 64 + lane] = gba[f2];
+      if constexpr (MODE != MODE_ADD) {
+        const double v = gbm[f2] + shfl_xor_f64<32>(gbm[f2]);
+        if (lane < 32) gw[f2 * 32 + lane] = v;
+      }
+      if constexpr (MODE != MODE_MULT) {
+        const double v = gba[f2] + shfl_xor_f64<32>(gba[f2]);
+        if (lane < 32) gw[((MODE == MODE_MIXED ? KMAX : 0) + f2) * 32 + lane] = v;
+      }
     }
   }
   __syncthreads();
   {
-    // feature f handled by 8 threads, each summing NW*8 partials
+    // feature f handled by 8 threads, each summing NW*4 partials
     constexpr int NSET = (MODE == MODE_MIXED) ? 2 : 1;
     const int tid = threadIdx.x;
     for (int job = tid; job < NSET * KMAX * 8; job += NW * 64) {
@@ -483,9 +541,11 @@ __device__ bool eval_collective(const FitKArgs &a, FitSmem<NW, KMAX> &sm, double
       const int f2 = fs % KMAX;
       double acc = 0.0;
       for (int w2 = 0; w2 < NW; ++w2) {
-        const double *src = sm.gbt + ((size_t)w2 * 2 * KMAX + set * KMAX + f2) * 64 + part * 8;
+        constexpr int NS2 = (MODE == MODE_MIXED) ? 2 : 1;
+        const int sset = (MODE == MODE_MIXED) ? set : 0;
+        const double *src = sm.gbt + ((size_t)w2 * NS2 * KMAX + sset * KMAX + f2) * 32 + part * 4;
 #pragma unroll
-        for (int q = 0; q < 8; ++q) acc += src[q];
+        for (int q = 0; q < 4; ++q) acc += src[q];
       }
       acc += shfl_xor_f64<1>(acc);
       acc += shfl_xor_f64<2>(acc);
@@ -494,6 +554,7 @@ __device__ bool eval_collective(const FitKArgs &a, FitSmem<NW, KMAX> &sm, double
     }
   }
   __syncthreads();
+  PF_STAMP(3);
   // ---- phase 3: wave 0 assembles f and g
   if (wave == 0) {
     double rrt = 0.0;
@@ -582,11 +643,12 @@ __device__ bool eval_collective(const FitKArgs &a, FitSmem<NW, KMAX> &sm, double
   g = sm.gout[lane];
   const bool bad = sm.fout[1] != 0.0;
   __syncthreads();
+  PF_STAMP(4);
   return bad;
 }
 
-template <int NW, int KMAX>
-__device__ __forceinline__ void load_y(const FitKArgs &a, FitSmem<NW, KMAX> &sm, int s) {
+template <int NW, int KMAX, int MODE>
+__device__ __forceinline__ void load_y(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, int s) {
   const double *ys = a.y_scaled + (size_t)s * a.Tp;
   for (int i = threadIdx.x; i < a.Tp; i += NW * 64) sm.y[i] = ys[i];
 }
@@ -595,10 +657,10 @@ __device__ __forceinline__ void load_y(const FitKArgs &a, FitSmem<NW, KMAX> &sm,
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
 __global__ __launch_bounds__(NW * 64) void k_objgrad(FitKArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  FitSmem<NW, KMAX> sm;
-  sm.carve(smem_raw, a.Tp, a.NB);
+  FitSmem<NW, KMAX, MODE> sm;
+  sm.carve(smem_raw, a.Tp, a.NB, a.P);
   const int s = blockIdx.x, lane = pf_lane();
-  load_y(a, sm, s);
+  load_y<NW, KMAX, MODE>(a, sm, s);
   const double x = (lane < a.P) ? a.theta[(size_t)s * a.P + lane] : 0.0;
   __syncthreads();
   double f, g;
@@ -655,17 +717,26 @@ struct LbScalars {
   double fk, fk1, fq, alpha, alphak_1, gammak;
   double dfp, c1dfp, c2dfp, alpha0, alpha1, prevF, prevDFp;
   double alo, aloF, aloDFp, ahi, ahiF, ahiDFp;
-  int itNum, resetB, nits, lsRestarts, zit, hcount, ret, n_eval;
+  double lastDFp;   // g_k . p_{k-1}  (directional derivative at acceptance)
+  double dfp_prev;  // g_{k-1} . p_{k-1} (dfp of the accepted line search)
+  double dfp_next;  // g_k . p_k = -g' H g of the new direction
+  int itNum, resetB, nits, lsRestarts, zit, hcount, ret, n_eval, head;
 };
 
 __device__ __forceinline__ double ddot(double u, double v) { return wave_sum(u * v); }
+// (a mod H) for 0 <= a < 2H without an integer division
+__device__ __forceinline__ int pf_wrap(int a, int H) {
+  a = (a >= H) ? a - H : a;
+  return (a >= H) ? a - H : a;
+}
 
 // Optimizer state kept in LDS (wave 0 only) so it does not compete with the
 // evaluation's registers.
 struct LbLds {
-  double xk[64], gk[64], pk[64], xk1[64], gk1[64], pk1[64];
-  double hs[PF_HIST][64], hy[PF_HIST][64];
-  double hrho[PF_HIST];
+  double xk[64], gk[64], pk[64];
+  double hs[PF_HIST][64], hy[PF_HIST][64];   // circular, logical j at (head + j) % H
+  double SY[PF_HIST][PF_HIST];                // s_i . y_j (logical order; upper part used)
+  double YY[PF_HIST][PF_HIST];                // y_i . y_j
   LbScalars z;
   int state;
   int need;
@@ -674,14 +745,11 @@ struct LbLds {
 // Advance the machine until it needs an evaluation (returns true, trial point
 // in xq) or terminates (returns false).  `bad` / fq / gq are the result of the
 // evaluation requested last time.
-__device__ __forceinline__ bool lbfgs_advance(const pf_fit_opts &o, LbLds &L, double &xq, double gq, bool bad) {
+__device__ __forceinline__ bool lbfgs_step(const pf_fit_opts &o, LbLds &L, int &state, LbScalars &z,
+                                           double &xk, double &gk, double &pk, double &xq, double gq,
+                                           bool bad) {
   const int lane = pf_lane();
   const int H = o.history < PF_HIST ? o.history : PF_HIST;
-  int &state = L.state;
-  LbScalars &z = L.z;
-  double &xk = L.xk[lane], &gk = L.gk[lane], &pk = L.pk[lane];
-  double &xk1 = L.xk1[lane], &gk1 = L.gk1[lane], &pk1 = L.pk1[lane];
-  double *hrho = L.hrho;
   while (true) {
     switch (state) {
       case LB_INIT:
@@ -690,6 +758,8 @@ __device__ __forceinline__ bool lbfgs_advance(const pf_fit_opts &o, LbLds &L, do
         gk = gq;
         pk = -gk;
         z.itNum = 0;
+        z.hcount = 0;
+        z.head = 0;
         state = LB_NEW_ITER;
         break;
       case LB_NEW_ITER:
@@ -698,14 +768,19 @@ __device__ __forceinline__ bool lbfgs_advance(const pf_fit_opts &o, LbLds &L, do
         state = LB_LS_START;
         break;
       case LB_LS_START:
-        if (z.resetB) pk = -gk;
         if (z.itNum > 1 && z.resetB != 2) {
-          z.alpha = fmin(1.0, 1.01 * cubic_interp0(ddot(gk1, pk1), z.alphak_1, z.fk - z.fk1,
-                                                   ddot(gk, pk1), 1e-12, 1.0));
+          // Stan: CubicInterp(g_{k-1}.p_{k-1}, alpha_{k-1}, f_k - f_{k-1}, g_k.p_{k-1})
+          z.alpha = fmin(1.0, 1.01 * cubic_interp0(z.dfp_prev, z.alphak_1, z.fk - z.fk1, z.lastDFp,
+                                                   1e-12, 1.0));
         } else {
           z.alpha = o.init_alpha;
         }
-        z.dfp = ddot(gk, pk);
+        if (z.resetB) {
+          pk = -gk;
+          z.dfp = ddot(gk, pk);
+        } else {
+          z.dfp = z.dfp_next;
+        }
         z.c1dfp = 1e-4 * z.dfp;
         z.c2dfp = 0.9 * z.dfp;
         z.alpha0 = 1e-12;
@@ -739,6 +814,7 @@ __device__ __forceinline__ bool lbfgs_advance(const pf_fit_opts &o, LbLds &L, do
           state = LB_ZOOM_ITER;
         } else if (fabs(newDFp) <= -z.c2dfp) {
           z.alpha = z.alpha1;
+          z.lastDFp = newDFp;
           state = LB_LS_OK;
         } else if (newDFp >= 0) {
           z.alo = z.alpha1; z.aloF = f1; z.aloDFp = newDFp;
@@ -784,7 +860,7 @@ __device__ __forceinline__ bool lbfgs_advance(const pf_fit_opts &o, LbLds &L, do
           z.ahi = z.alpha; z.ahiF = f1; z.ahiDFp = newDFp;
           state = LB_ZOOM_ITER;
         } else {
-          if (fabs(newDFp) <= -z.c2dfp) { state = LB_LS_OK; break; }
+          if (fabs(newDFp) <= -z.c2dfp) { z.lastDFp = newDFp; state = LB_LS_OK; break; }
           if (newDFp * (z.ahi - z.alo) >= 0) { z.ahi = z.alo; z.ahiF = z.aloF; z.ahiDFp = z.aloDFp; }
           z.alo = z.alpha; z.aloF = f1; z.aloDFp = newDFp;
           state = LB_ZOOM_ITER;
@@ -797,19 +873,49 @@ __device__ __forceinline__ bool lbfgs_advance(const pf_fit_opts &o, LbLds &L, do
         state = LB_LS_START;
         break;
       case LB_LS_OK: {
-        // accepted point = last evaluated (xq, fq, gq); swap so k is the newest
+        PF_STAMP(10);
+        // accepted point = last evaluated (xq, fq, gq); k becomes the newest
         z.fk1 = z.fk;
         z.fk = z.fq;
-        xk1 = xk; xk = xq;
-        gk1 = gk; gk = gq;
-        pk1 = pk;
-        const double sk = xk - xk1, yk = gk - gk1;
+        const double sk = xq - xk, yk = gq - gk;
+        xk = xq;
+        gk = gq;
         z.alphak_1 = z.alpha;
+        z.dfp_prev = z.dfp;
+        // LBFGSUpdate history after this update: clear on reset, drop the
+        // oldest pair when full; kept pairs are old logical j + drop
+        const int m_old = z.resetB ? 0 : z.hcount;
+        const int drop = (m_old == H) ? 1 : 0;
+        const int nw = m_old - drop;  // logical index of the new pair
+        // one fused reduction for every inner product this step needs
+        double v[22], r[22];
+        v[0] = gq * gq;
+        v[1] = sk * sk;
+        v[2] = sk * yk;
+        v[3] = yk * yk;
+#pragma unroll
+        for (int j = 0; j < PF_HIST - 1; ++j) {
+          double sj = 0.0, yj = 0.0;
+          if (j < nw) {
+            const int slot = pf_wrap(z.head + j + drop, H);
+            sj = L.hs[slot][lane];
+            yj = L.hy[slot][lane];
+          }
+          v[4 + 2 * j] = sj * yk;
+          v[5 + 2 * j] = yj * yk;
+          v[12 + 2 * j] = sj * gq;
+          v[13 + 2 * j] = yj * gq;
+        }
+        v[20] = sk * gq;
+        v[21] = yk * gq;
+        wave_sum_multi<22>(v, r);
+        PF_STAMP(11);
+        const double gg = r[0];
         if (fabs(z.fk1 - z.fk) < o.tol_obj) {
           z.ret = PF_ST_ABSF;
-        } else if (sqrt(ddot(gk, gk)) < o.tol_grad) {
+        } else if (sqrt(gg) < o.tol_grad) {
           z.ret = PF_ST_ABSGRAD;
-        } else if (sqrt(ddot(sk, sk)) < o.tol_param) {
+        } else if (sqrt(r[1]) < o.tol_param) {
           z.ret = PF_ST_ABSX;
         } else if (z.itNum >= o.max_iter) {
           z.ret = PF_ST_MAXIT;
@@ -817,46 +923,100 @@ __device__ __forceinline__ bool lbfgs_advance(const pf_fit_opts &o, LbLds &L, do
                    o.tol_rel_obj * 2.220446049250313e-16) {
           z.ret = PF_ST_RELF;
         } else {
-          const double skyk = ddot(yk, sk);
-          if (z.resetB) z.hcount = 0;
-          z.gammak = skyk / ddot(yk, yk);
-          if (z.hcount == H) {
+          // ---- LBFGSUpdate::update, compact form (Byrd-Nocedal-Schnabel):
+          //      H g = gamma g + S p' - gamma Y u,  u = R^-1 a,
+          //      p' = R^-T ((D + gamma Y'Y) u - gamma b),  a = S'g, b = Y'g,
+          //      R = upper(S'Y), D = diag(S'Y), gamma = s'y / y'y (newest pair).
+          //      Identical to Stan's two-loop recursion in exact arithmetic.
+          z.gammak = r[2] / r[3];
+          const double gam = z.gammak;
+          // small matrices in registers for this step (static indices)
+          double SYr[PF_HIST][PF_HIST], YYr[PF_HIST][PF_HIST];
 #pragma unroll
-            for (int q = 0; q < PF_HIST - 1; ++q)
-              if (q < H - 1) {
-                L.hs[q][lane] = L.hs[q + 1][lane];
-                L.hy[q][lane] = L.hy[q + 1][lane];
-                if (lane == 0) hrho[q] = hrho[q + 1];
+          for (int i = 0; i < PF_HIST; ++i)
+#pragma unroll
+            for (int j = 0; j < PF_HIST; ++j) {
+              const int ii = (i + drop < PF_HIST) ? i + drop : PF_HIST - 1;
+              const int jj = (j + drop < PF_HIST) ? j + drop : PF_HIST - 1;
+              SYr[i][j] = L.SY[ii][jj];
+              YYr[i][j] = L.YY[ii][jj];
+            }
+          if (drop) z.head = pf_wrap(z.head + 1, H);
+          const int slot_new = pf_wrap(z.head + nw, H);
+          L.hs[slot_new][lane] = sk;
+          L.hy[slot_new][lane] = yk;
+#pragma unroll
+          for (int j = 0; j < PF_HIST; ++j) {
+            if (j < nw) {
+              // column nw of R and row/col nw of Y'Y (static j, runtime nw)
+#pragma unroll
+              for (int q = 0; q < PF_HIST; ++q) {
+                if (q == nw) {
+                  SYr[j][q] = r[4 + 2 * j];
+                  YYr[j][q] = r[5 + 2 * j];
+                  YYr[q][j] = r[5 + 2 * j];
+                }
               }
-            z.hcount = H - 1;
+            }
           }
 #pragma unroll
           for (int q = 0; q < PF_HIST; ++q)
-            if (q == z.hcount) {
-              L.hs[q][lane] = sk;
-              L.hy[q][lane] = yk;
-              if (lane == 0) hrho[q] = 1.0 / skyk;
-            }
-          z.hcount++;
-          double al[PF_HIST];
-          pk = -gk;
+            if (q == nw) { SYr[q][q] = r[2]; YYr[q][q] = r[3]; }
+          if (lane == 0) {
 #pragma unroll
-          for (int q = PF_HIST - 1; q >= 0; --q) {
-            al[q] = 0.0;
-            if (q < z.hcount) {
-              al[q] = hrho[q] * ddot(L.hs[q][lane], pk);
-              pk -= al[q] * L.hy[q][lane];
+            for (int i = 0; i < PF_HIST; ++i)
+#pragma unroll
+              for (int j = 0; j < PF_HIST; ++j) { L.SY[i][j] = SYr[i][j]; L.YY[i][j] = YYr[i][j]; }
+          }
+          const int m = nw + 1;
+          z.hcount = m;
+          double av[PF_HIST], bv[PF_HIST], uu[PF_HIST], pp[PF_HIST];
+#pragma unroll
+          for (int j = 0; j < PF_HIST; ++j) {
+            av[j] = (j < nw) ? r[12 + 2 * j] : ((j == nw) ? r[20] : 0.0);
+            bv[j] = (j < nw) ? r[13 + 2 * j] : ((j == nw) ? r[21] : 0.0);
+            uu[j] = 0.0;
+            pp[j] = 0.0;
+          }
+          // u = R^-1 a (back substitution)
+#pragma unroll
+          for (int i = PF_HIST - 1; i >= 0; --i) {
+            if (i < m) {
+              double t = av[i];
+#pragma unroll
+              for (int j = i + 1; j < PF_HIST; ++j)
+                if (j < m) t -= SYr[i][j] * uu[j];
+              uu[i] = t / SYr[i][i];
             }
           }
-          pk *= z.gammak;
+          // w = (D + gamma Y'Y) u - gamma b ; p' = R^-T w (forward substitution)
 #pragma unroll
-          for (int q = 0; q < PF_HIST; ++q) {
-            if (q < z.hcount) {
-              const double bq = hrho[q] * ddot(L.hy[q][lane], pk);
-              pk += (al[q] - bq) * L.hs[q][lane];
+          for (int i = 0; i < PF_HIST; ++i) {
+            if (i < m) {
+              double w = SYr[i][i] * uu[i] - gam * bv[i];
+#pragma unroll
+              for (int j = 0; j < PF_HIST; ++j)
+                if (j < m) w += gam * YYr[i][j] * uu[j];
+#pragma unroll
+              for (int j = 0; j < PF_HIST; ++j)
+                if (j < i) w -= SYr[j][i] * pp[j];
+              pp[i] = w / SYr[i][i];
             }
           }
-          if (-ddot(pk, gk) / fmax(fabs(z.fk), 1.0) < o.tol_rel_grad * 2.220446049250313e-16)
+          double Hg = gam * gq;
+          double gHg = gam * gg;
+#pragma unroll
+          for (int j = 0; j < PF_HIST; ++j) {
+            if (j < m) {
+              const int slot = pf_wrap(z.head + j, H);
+              Hg += pp[j] * L.hs[slot][lane] - gam * uu[j] * L.hy[slot][lane];
+              gHg += pp[j] * av[j] - gam * uu[j] * bv[j];
+            }
+          }
+          pk = -Hg;
+          z.dfp_next = -gHg;
+          PF_STAMP(12);
+          if (gHg / fmax(fabs(z.fk), 1.0) < o.tol_rel_grad * 2.220446049250313e-16)
             z.ret = PF_ST_RELGRAD;
           else
             z.ret = PF_ST_SUCCESS;
@@ -871,6 +1031,29 @@ __device__ __forceinline__ bool lbfgs_advance(const pf_fit_opts &o, LbLds &L, do
   }
 }
 
+
+// State lives in LDS between evaluations; copy it into registers for the
+// step (one batch of independent LDS loads) and write it back at the end.
+__device__ __forceinline__ bool lbfgs_advance(const pf_fit_opts &o, LbLds &L, double &xq, double gq,
+                                              bool bad) {
+  const int lane = pf_lane();
+  PF_STAMP(6);
+  LbScalars z = L.z;
+  int state = L.state;
+  double xk = L.xk[lane], gk = L.gk[lane], pk = L.pk[lane];
+  PF_STAMP(7);
+  const bool need = lbfgs_step(o, L, state, z, xk, gk, pk, xq, gq, bad);
+  PF_STAMP(8);
+  L.xk[lane] = xk;
+  L.gk[lane] = gk;
+  L.pk[lane] = pk;
+  if (lane == 0) {
+    L.z = z;
+    L.state = state;
+  }
+  return need;
+}
+
 static_assert(sizeof(LbLds) + 16 <= kLbBytes, "LbLds too big");
 
 #include "pf_polish.h"
@@ -879,8 +1062,8 @@ static_assert(sizeof(LbLds) + 16 <= kLbBytes, "LbLds too big");
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
 __global__ __launch_bounds__(NW * 64, 2) void k_fit(FitKArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  FitSmem<NW, KMAX> sm;
-  sm.carve(smem_raw, a.Tp, a.NB);
+  FitSmem<NW, KMAX, MODE> sm;
+  sm.carve(smem_raw, a.Tp, a.NB, a.P);
   const int s = blockIdx.x, lane = pf_lane();
   const int P = a.P;
   double *th_out = a.theta + (size_t)s * P;
@@ -896,7 +1079,7 @@ __global__ __launch_bounds__(NW * 64, 2) void k_fit(FitKArgs a) {
     }
     return;
   }
-  load_y(a, sm, s);
+  load_y<NW, KMAX, MODE>(a, sm, s);
   LbLds &L = *sm.lb;
   double xq = (lane < P) ? th_out[lane] : 0.0;
   if (pf_wave() == 0) {
@@ -905,7 +1088,6 @@ __global__ __launch_bounds__(NW * 64, 2) void k_fit(FitKArgs a) {
     if (lane == 0) memset(&L.z, 0, sizeof(LbScalars));
 #pragma unroll
     for (int q = 0; q < PF_HIST; ++q) { L.hs[q][lane] = 0.0; L.hy[q][lane] = 0.0; }
-    if (lane < PF_HIST) L.hrho[lane] = 0.0;
   }
   __syncthreads();
   // ---- phase A: Stan-faithful L-BFGS (reverse communication)
@@ -915,31 +1097,64 @@ __global__ __launch_bounds__(NW * 64, 2) void k_fit(FitKArgs a) {
     const bool bad = eval_collective<NW, KMAX, O0, O1, O2, MODE>(a, sm, xq, fq, gq);
     ++n_eval;
     if (pf_wave() == 0) {
-      L.z.fq = fq;
+      if (lane == 0) L.z.fq = fq;
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
       const bool need = lbfgs_advance(a.o, L, xq, gq, bad);
       if (lane == 0) L.need = need ? 1 : 0;
     }
     __syncthreads();
     const int need = L.need;
     __syncthreads();
+    PF_STAMP(5);
     if (!need) break;
   }
   double xk = L.xk[lane];
   double gk = L.gk[lane];
   double f = L.z.fk;
   const double f_stan = f;
-  // ---- phase B: exact-MAP polish (engine extension, see pf_polish.h)
-  if (a.o.polish && L.z.ret != PF_ST_BADINIT && a.growth == PF_GROWTH_LINEAR) {
-    polish_run<NW, KMAX, O0, O1, O2, MODE>(a, sm, xk, f, gk, n_eval);
-  }
+  const int st_stan = L.z.ret, it_stan = L.z.itNum;
+  int n_newton = 0;
+  (void)n_newton;
   if (threadIdx.x < 64) {
     if (lane < P) th_out[lane] = xk;
     if (lane == 0) {
       a.f_out[s] = f;
       a.f_stan[s] = f_stan;
-      a.status[s] = L.z.ret;
-      a.n_iter[s] = L.z.itNum;
+      a.status[s] = st_stan;
+      a.n_iter[s] = it_stan;
       a.n_eval[s] = n_eval;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- K3b polish kernel
+// Separate launch so the Hessian's MFMA accumulators get their own register
+// budget (the L-BFGS kernel stays at 2 waves/SIMD).  Reads the Stan-phase
+// optimum from theta, re-evaluates f/g there, runs the proximal-Newton polish.
+template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
+__global__ __launch_bounds__(NW * 64, 2) void k_polish(FitKArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  FitSmem<NW, KMAX, MODE> sm;
+  sm.carve(smem_raw, a.Tp, a.NB, a.P);
+  const int s = blockIdx.x, lane = pf_lane();
+  const int P = a.P;
+  const int st = a.status[s];
+  if (st == PF_ST_CONSTANT || st == PF_ST_BADINIT) return;
+  double *th_out = a.theta + (size_t)s * P;
+  load_y<NW, KMAX, MODE>(a, sm, s);
+  double x = (lane < P) ? th_out[lane] : 0.0;
+  __syncthreads();
+  double f, g;
+  const bool bad = eval_collective<NW, KMAX, O0, O1, O2, MODE>(a, sm, x, f, g);
+  if (bad) return;
+  int n_eval = 1, n_newton = 0;
+  polish_run<NW, KMAX, O0, O1, O2, MODE>(a, sm, x, f, g, n_eval, n_newton);
+  if (threadIdx.x < 64) {
+    if (lane < P) th_out[lane] = x;
+    if (lane == 0) {
+      a.f_out[s] = f;
+      a.n_eval[s] += n_eval;
     }
   }
 }
@@ -966,7 +1181,7 @@ struct PredKArgs {
 // k-th and (k+1)-th smallest of the wave's samples (v[q] = +inf if absent).
 // Fast path: bound from the (k+2)-th smallest per-lane minimum, compact the
 // candidates into LDS, bitonic-sort 64.  Fallback: exact bit-bisection.
-__device__ __noinline__ void wave_select_pair(const float (&v)[PF_NQ], int k, float *buf, float &a, float &b) {
+__device__ __forceinline__ void wave_select_pair(const float (&v)[PF_NQ], int k, float *buf, float &a, float &b) {
   const int lane = pf_lane();
   float lmin = INFINITY;
 #pragma unroll
@@ -1026,18 +1241,19 @@ __device__ __forceinline__ float np_lerp(float a, float b, float t) {
 
 // trend offset of MC sample `smp` at time ti (in scaled units):
 // sum over the sample's new changepoints with ti >= t_c of delta_c (ti - t_c)
-__device__ __noinline__ double mc_trend_offset(const PredKArgs &a, int series, int smp,
-                                                  double ti, double lam) {
+__device__ __noinline__ double mc_trend_offset(uint32_t seed0, uint32_t seed1, double lam_pois,
+                                               double t_max, int series, int smp, double ti,
+                                               double lam) {
   const pf_u4 r0 = philox4x32_10(pf_u4{(uint32_t)smp, 0u, (uint32_t)series, 0x7EE2D00Du},
-                                 a.seed0 ^ 0x5A5A5A5Au, a.seed1);
+                                 seed0 ^ 0x5A5A5A5Au, seed1);
   // Poisson(lam_pois) by inversion
   const double u0 = pf_u01d(r0.x, r0.y);
   int n = 0;
-  if (a.lam_pois > 0.0) {
-    double p = exp(-a.lam_pois), F = p;
+  if (lam_pois > 0.0) {
+    double p = exp(-lam_pois), F = p;
     while (u0 > F && n < 100000) {
       ++n;
-      p *= a.lam_pois / (double)n;
+      p *= lam_pois / (double)n;
       F += p;
       if (p == 0.0 && F < u0) break;
     }
@@ -1046,8 +1262,8 @@ __device__ __noinline__ double mc_trend_offset(const PredKArgs &a, int series, i
   for (int c = 0; c < n; ++c) {
     const pf_u4 rc = philox4x32_10(pf_u4{(uint32_t)smp, (uint32_t)(c + 1), (uint32_t)series,
                                          0x7EE2D00Du},
-                                   a.seed0 ^ 0x5A5A5A5Au, a.seed1);
-    const double tc = 1.0 + pf_u01d(rc.x, rc.y) * (a.t_max - 1.0);
+                                   seed0 ^ 0x5A5A5A5Au, seed1);
+    const double tc = 1.0 + pf_u01d(rc.x, rc.y) * (t_max - 1.0);
     const double ul = pf_u01d(rc.z, rc.w);
     const double lap = (ul >= 0.5) ? -lam * log(2.0 - ul - ul) : lam * log(ul + ul);
     if (ti >= tc) off += lap * (ti - tc);
@@ -1140,7 +1356,7 @@ __global__ __launch_bounds__(256) void k_predict(PredKArgs a) {
 #pragma unroll 1
         for (int q = 0; q < PF_NQ; ++q) {
           const int smp = lane + 64 * q;
-          offs[q * 64 + lane] = (smp < a.N) ? (float)(ysc * mc_trend_offset(a, series, smp, ti, lam)) : 0.0f;
+          offs[q * 64 + lane] = (smp < a.N) ? (float)(ysc * mc_trend_offset(a.seed0, a.seed1, a.lam_pois, a.t_max, series, smp, ti, lam)) : 0.0f;
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -1200,6 +1416,8 @@ int pf_ctx_create(int device, pf_ctx **out) {
   pf_ctx *c = new pf_ctx();
   c->device = device;
   c->err[0] = 0;
+  c->ws = nullptr;
+  c->ws_bytes = 0;
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess) {
     snprintf(g_err_noctx, sizeof g_err_noctx, "hipSetDevice(%d): %s", device, hipGetErrorString(e));
@@ -1210,8 +1428,34 @@ int pf_ctx_create(int device, pf_ctx **out) {
   return 0;
 }
 
+#ifdef PF_STAMPS
+int pf_debug_stamps(unsigned long long *out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pf_dbg), sizeof(unsigned long long) * 32) != hipSuccess) return -2;
+  if (reset) {
+    unsigned long long z[32] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(pf_dbg), z, sizeof z) != hipSuccess) return -2;
+  }
+  return 0;
+}
+#endif
+
 int pf_ctx_destroy(pf_ctx *ctx) {
+  if (ctx && ctx->ws) (void)hipFree(ctx->ws);
   delete ctx;
+  return 0;
+}
+
+// grow the context scratch (synchronises the device when it has to grow;
+// steady-state calls with the same shapes never allocate)
+static int ctx_workspace(pf_ctx *ctx, size_t bytes, void **out) {
+  if (bytes > ctx->ws_bytes) {
+    if (ctx->ws) PF_HIP(ctx, hipFree(ctx->ws));
+    ctx->ws = nullptr;
+    ctx->ws_bytes = 0;
+    PF_HIP(ctx, hipMalloc(&ctx->ws, bytes));
+    ctx->ws_bytes = bytes;
+  }
+  *out = ctx->ws;
   return 0;
 }
 
@@ -1321,13 +1565,20 @@ FitKArgs make_fit_args(const pf_problem *pb) {
 
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
 int launch_fitlike(pf_ctx *ctx, bool fit, const FitKArgs &a, int n, hipStream_t st) {
-  const size_t smem = FitSmem<NW, KMAX>::bytes(a.Tp, a.NB);
+  const size_t smem = FitSmem<NW, KMAX, MODE>::bytes(a.Tp, a.NB, a.P);
   if (smem > 160 * 1024) return set_err(ctx, "fit: series too long for the LDS budget");
   if (fit) {
     auto kern = k_fit<NW, KMAX, O0, O1, O2, MODE>;
     PF_HIP(ctx, hipFuncSetAttribute((const void *)kern,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
     hipLaunchKernelGGL(kern, dim3(n), dim3(NW * 64), smem, st, a);
+    PF_HIP(ctx, hipGetLastError());
+    if (a.o.polish && a.ws && a.growth == PF_GROWTH_LINEAR && a.K <= 32 && 2 + a.S <= 32) {
+      auto kp = k_polish<NW, KMAX, O0, O1, O2, MODE>;
+      PF_HIP(ctx, hipFuncSetAttribute((const void *)kp,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+      hipLaunchKernelGGL(kp, dim3(n), dim3(NW * 64), smem, st, a);
+    }
   } else {
     auto kern = k_objgrad<NW, KMAX, O0, O1, O2, MODE>;
     PF_HIP(ctx, hipFuncSetAttribute((const void *)kern,
@@ -1408,6 +1659,13 @@ int pf_fit(pf_ctx *ctx, const pf_problem *pb, const pf_fit_opts *opts, double *t
   a.n_iter = n_iter;
   a.n_eval = n_eval;
   a.o = *opts;
+  a.ws = nullptr;
+  if (opts->polish) {
+    void *w = nullptr;
+    const int rc2 = ctx_workspace(ctx, (size_t)pb->n_series * 3 * pb->grid.T_pad * sizeof(double), &w);
+    if (rc2) return rc2;
+    a.ws = (double *)w;
+  }
   return dispatch_fitlike(ctx, true, a, pb->n_series, is_fourier103(pb), mode_of(pb),
                           (hipStream_t)stream);
 }

@@ -1,7 +1,377 @@
-// pf_polish.h — exact-MAP proximal-Newton polish (stub; filled in next)
+// pf_polish.h — exact-MAP polish after the Stan-faithful L-BFGS phase.
+//
+// Engine extension (NOT part of Stan): Stan's smooth L-BFGS stalls at the L1
+// kink of delta ~ double_exponential(0, tau) up to ~3e-5 relative short of the
+// MAP (yhat off by up to ~2e-3*y_scale).  From where it stops we run proximal
+// Newton on f = h + c*||delta||_1 (c = 1/tau):
+//   1. exact Hessian of the smooth part h.  Its data term (J^T J - R)/sigma^2
+//      is a genuine GEMM over the T rows: J[T x 64] with 10 16x16 output tiles,
+//      accumulated on FP64 MFMA (v_mfma_f64_16x16x4f64);
+//   2. the lasso-QP subproblem min gh.d + d'Hd/2 + c||x_delta + d_delta||_1,
+//      solved exactly by an active-set method (Cholesky solves in LDS, wave 0);
+//   3. Armijo backtracking on the true objective (collective evaluations).
+// Same algorithm as oracle/stan_lbfgs.c:orc_polish (the CPU check).
+// Linear growth, K <= 32, 2 + S <= 32 (the reference configuration).
 #pragma once
+
+typedef double pf_d4 __attribute__((ext_vector_type(4)));
+
+#define PF_NTILE 10
+// tile (row block, col block) in the 64-column space [a: 0..31 | beta: 32..63]
+__device__ __forceinline__ int tile_ti(int q) {
+  constexpr int T_I[PF_NTILE] = {0, 0, 1, 2, 2, 3, 0, 0, 1, 1};
+  return T_I[q];
+}
+__device__ __forceinline__ int tile_tj(int q) {
+  constexpr int T_J[PF_NTILE] = {0, 1, 1, 2, 3, 3, 2, 3, 2, 3};
+  return T_J[q];
+}
+
+// column of the 64-wide J space -> parameter index (or -1)
+__device__ __forceinline__ int colmap(int c, int S, int K) {
+  if (c < 32) return (c < 2 + S) ? c : -1;
+  const int f = c - 32;
+  return (f < K) ? 3 + S + f : -1;
+}
+
+// publish theta (wave 0) — same as the evaluation's phase 0
+template <int NW, int KMAX, int MODE>
+__device__ __forceinline__ void publish_theta(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, double x);
+
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
-__device__ void polish_run(const FitKArgs &a, FitSmem<NW, KMAX> &sm, double &x, double &f,
-                           double &g, int &n_eval) {
-  (void)a; (void)sm; (void)x; (void)f; (void)g; (void)n_eval;
+__device__ __forceinline__ void hessian_collective(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, double x,
+                                   double gh, double *ws) {
+  const int lane = pf_lane(), wave = pf_wave();
+  const int S = a.S, K = a.K, T = a.T, Tp = a.Tp, P = a.P;
+  publish_theta<NW, KMAX, MODE>(a, sm, x);
+  __syncthreads();
+  // ---- H1: per-row u, tr, r into the workspace (row per lane)
+  double Q = 0.0;
+  const double th_m = sm.th[1];
+  const bool linear = (a.growth == PF_GROWTH_LINEAR);
+  for (int b = wave; b < a.NB; b += NW) {
+    const int i = b * 64 + lane;
+    const bool valid = i < T;
+    RowIn cur;
+    load_row<O0, O1, O2>(a.t, a.seg, a.XT, Tp, i, cur);
+    double xf[KMAX];
+    row_features_from<KMAX, O0, O1, O2>(cur, a.XT, Tp, K, i, xf);
+    double xm[4] = {0.0, 0.0, 0.0, 0.0}, xa[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int f2 = 0; f2 < KMAX; ++f2) {
+      if constexpr (MODE != MODE_ADD) xm[f2 & 3] = fma(xf[f2], sm.bm[f2], xm[f2 & 3]);
+      if constexpr (MODE != MODE_MULT) xa[f2 & 3] = fma(xf[f2], sm.ba[f2], xa[f2 & 3]);
+      if ((f2 & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+    }
+    const double xbm = (xm[0] + xm[1]) + (xm[2] + xm[3]);
+    const double xba = (xa[0] + xa[1]) + (xa[2] + xa[3]);
+    const double tr = linear ? fma(sm.kseg[cur.seg], cur.t, sm.mseg[cur.seg]) : th_m;
+    const double u = 1.0 + xbm;
+    const double r = valid ? (sm.y[i] - fma(tr, u, xba)) : 0.0;
+    Q = fma(r, r, Q);
+    ws[i] = valid ? u : 0.0;
+    ws[Tp + i] = valid ? tr : 0.0;
+    ws[2 * Tp + i] = r;
+  }
+  Q = wave_sum(Q);
+  if (lane == 0) sm.rrw[wave] = Q;
+  __syncthreads();
+  // ---- H2: J^T J - R on FP64 MFMA.  k-steps of 4 rows, split over waves.
+  pf_d4 acc[PF_NTILE];
+#pragma unroll
+  for (int q = 0; q < PF_NTILE; ++q) acc[q] = pf_d4{0.0, 0.0, 0.0, 0.0};
+  const int c16 = lane & 15;
+  const int c1 = 16 + c16;
+  const double tc0 = (c16 >= 2 && c16 - 2 < S) ? a.t_change[c16 - 2] : 0.0;
+  const double tc1 = (c1 - 2 < S) ? a.t_change[c1 - 2] : 0.0;
+  const bool f2v = c16 < K, f3v = c1 < K;
+  const double cm2 = f2v ? a.s_m[c16] : 0.0, ca2 = f2v ? a.s_a[c16] : 0.0;
+  const double cm3 = f3v ? a.s_m[c1] : 0.0, ca3 = f3v ? a.s_a[c1] : 0.0;
+  const int nks = Tp >> 2;
+  for (int s = wave; s < nks; s += NW) {
+    const int rho = 4 * s + (lane >> 4);
+    const double u = ws[rho], tr = ws[Tp + rho], r = ws[2 * Tp + rho];
+    const double ti = a.t[rho];
+    const int sg = a.seg[rho];
+    // a columns (tile 0: c16, tile 1: 16 + c16)
+    double D0, D1;
+    if (c16 == 0) D0 = ti;
+    else if (c16 == 1) D0 = 1.0;
+    else D0 = (c16 - 2 < S && sg > c16 - 2) ? ti - tc0 : 0.0;
+    D1 = (c1 - 2 < S && sg > c1 - 2) ? ti - tc1 : 0.0;
+    if (rho >= T) { D0 = 0.0; D1 = 0.0; }
+    const double Du0 = D0 * u, Du1 = D1 * u;
+    // beta columns (tile 2: f = c16, tile 3: f = 16 + c16)
+    const double X2 = f2v ? a.XT[(size_t)c16 * Tp + rho] : 0.0;
+    const double X3 = f3v ? a.XT[(size_t)c1 * Tp + rho] : 0.0;
+    const double k2 = fma(tr, cm2, ca2), k3 = fma(tr, cm3, ca3);
+    const double V2 = X2 * k2, V3 = X3 * k3;
+    const double W2 = X2 * fma(u, k2, -r * cm2), W3 = X3 * fma(u, k3, -r * cm3);
+    acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(Du0, Du0, acc[0], 0, 0, 0);
+    acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(Du0, Du1, acc[1], 0, 0, 0);
+    acc[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(Du1, Du1, acc[2], 0, 0, 0);
+    acc[3] = __builtin_amdgcn_mfma_f64_16x16x4f64(V2, V2, acc[3], 0, 0, 0);
+    acc[4] = __builtin_amdgcn_mfma_f64_16x16x4f64(V2, V3, acc[4], 0, 0, 0);
+    acc[5] = __builtin_amdgcn_mfma_f64_16x16x4f64(V3, V3, acc[5], 0, 0, 0);
+    acc[6] = __builtin_amdgcn_mfma_f64_16x16x4f64(D0, W2, acc[6], 0, 0, 0);
+    acc[7] = __builtin_amdgcn_mfma_f64_16x16x4f64(D0, W3, acc[7], 0, 0, 0);
+    acc[8] = __builtin_amdgcn_mfma_f64_16x16x4f64(D1, W2, acc[8], 0, 0, 0);
+    acc[9] = __builtin_amdgcn_mfma_f64_16x16x4f64(D1, W3, acc[9], 0, 0, 0);
+  }
+  // ---- H3: chained reduction of the tiles over waves through one
+  // wave-sized LDS buffer (NW-1 hops; keeps the union region small)
+  double *red = sm.U;  // [PF_NTILE][4][64]
+  for (int w2 = NW - 1; w2 >= 1; --w2) {
+    if (wave == w2) {
+#pragma unroll
+      for (int q = 0; q < PF_NTILE; ++q)
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg) red[((size_t)q * 4 + rg) * 64 + lane] = acc[q][rg];
+    }
+    __syncthreads();
+    if (wave == w2 - 1) {
+#pragma unroll
+      for (int q = 0; q < PF_NTILE; ++q)
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg) acc[q][rg] += red[((size_t)q * 4 + rg) * 64 + lane];
+    }
+    __syncthreads();
+  }
+  // ---- H4: wave 0 assembles H (LDS, stride LD) incl. priors and the l row
+  if (wave == 0) {
+    double *H = sm.U;
+    const int LD = sm.LD;
+    for (int e = lane; e < P * LD; e += 64) H[e] = 0.0;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    Q = 0.0;
+    for (int w2 = 0; w2 < NW; ++w2) Q += sm.rrw[w2];
+    const double ls = readlane_f64(x, 2 + S);
+    const double sig2 = exp(2.0 * ls);
+    const double inv = 1.0 / sig2;
+#pragma unroll
+    for (int q = 0; q < PF_NTILE; ++q) {
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        const int ci = tile_ti(q) * 16 + (lane >> 4) + 4 * rg;
+        const int cj = tile_tj(q) * 16 + (lane & 15);
+        const int pi = colmap(ci, S, K), pj = colmap(cj, S, K);
+        if (pi >= 0 && pj >= 0) {
+          const double v = acc[q][rg] * inv;
+          H[pi * LD + pj] = v;
+          H[pj * LD + pi] = v;
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // priors, l row/col: d2h/dl2 = 8 sigma^2 + 2Q/sigma^2;
+    // d2h/dl dp = (2/sigma^2) sum r dmu/dp = -2 (gh_p - prior'_p)
+    const int il = 2 + S;
+    const int p = lane;
+    if (p < P) {
+      double prior1 = 0.0, prior2 = 0.0;
+      if (p == 0 || p == 1) { prior1 = x / 25.0; prior2 = 1.0 / 25.0; }
+      else if (p > il) {
+        const double sg2 = a.sigmas[p - il - 1];
+        prior1 = x / (sg2 * sg2);
+        prior2 = 1.0 / (sg2 * sg2);
+      }
+      if (p != il) {
+        H[p * LD + p] += prior2;
+        const double v = -2.0 * (gh - prior1);
+        H[il * LD + p] = v;
+        H[p * LD + il] = v;
+      } else {
+        H[il * LD + il] = 8.0 * sig2 + 2.0 * Q * inv;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// Cholesky (right-looking, lane = column of the trailing square) + solve,
+// wave-local.  M (n x n, stride LD) overwritten by L; b (lane i = b_i) -> x.
+__device__ __forceinline__ bool wave_chol_solve(double *M, int LD, int n, double &b) {
+  const int lane = pf_lane();
+  for (int k = 0; k < n; ++k) {
+    const double d = M[k * LD + k];
+    if (!(d > 0.0)) return false;
+    const double Lkk = sqrt(d);
+    double Ljk = 0.0;
+    if (lane > k && lane < n) {
+      Ljk = M[lane * LD + k] / Lkk;
+      M[lane * LD + k] = Ljk;
+    }
+    if (lane == k) M[k * LD + k] = Lkk;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (lane > k && lane < n) {
+      for (int i = k + 1; i < n; ++i) M[i * LD + lane] -= M[i * LD + k] * Ljk;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  // forward: L y = b
+  for (int k = 0; k < n; ++k) {
+    const double yk = readlane_f64(b, k) / M[k * LD + k];
+    if (lane == k) b = yk;
+    if (lane > k && lane < n) b -= M[lane * LD + k] * yk;
+  }
+  // backward: L^T x = y
+  for (int k = n - 1; k >= 0; --k) {
+    const double xk = readlane_f64(b, k) / M[k * LD + k];
+    if (lane == k) b = xk;
+    if (lane < k) b -= M[k * LD + lane] * xk;
+  }
+  return true;
+}
+
+// Active-set solution of min gh.(z-x) + (z-x)'H(z-x)/2 + c||z_delta||_1 (wave 0).
+// Returns z in lane p; false if a factorisation failed.
+template <int NW, int KMAX, int MODE>
+__device__ __forceinline__ bool qp_active(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, double x, double gh, double c,
+                          double &z, int &nsolve) {
+  const int lane = pf_lane();
+  const int P = a.P, S = a.S, LD = sm.LD;
+  const double *H = sm.U;
+  double *M = sm.U + (size_t)P * LD;
+  int *map = sm.qmap;
+  const bool isd = (lane >= 2 && lane < 2 + S);
+  bool zero = false;
+  double sgn_ = 0.0;
+  if (isd) {
+    const double sgx = (x > 0.0) - (x < 0.0), sgg = (gh > 0.0) - (gh < 0.0);
+    if (fabs(gh) <= c) zero = true;
+    else if (x != 0.0 && sgx == -sgg) sgn_ = sgx;
+    else sgn_ = -sgg;
+  }
+  z = x;
+  const int max_as = 2 * S + 16;
+  for (int it = 0; it < max_as; ++it) {
+    const bool fr = (lane < P) && !zero;
+    const unsigned long long fm = __ballot(fr);
+    const int n = __popcll(fm);
+    const int pos = __popcll(fm & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
+    if (fr) map[pos] = lane;
+    // dz for zero coords: (0 - x_q) ; x_q of zero coords enters the rhs
+    sm.pz[lane] = (lane < P && zero) ? x : 0.0;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    double rhs = 0.0;
+    if (lane < n) {
+      const int pa = map[lane];
+      double v = 0.0;
+      for (int q = 0; q < P; ++q) v += H[pa * LD + q] * sm.pz[q];
+      rhs = v;
+      for (int b = 0; b < n; ++b) M[lane * LD + b] = H[pa * LD + map[b]];
+    }
+    // -(gh + c s) of the free coordinate at position `lane`
+    const double own = -(gh + c * sgn_);
+    sm.pd[lane] = own;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (lane < n) rhs += sm.pd[map[lane]];
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (!wave_chol_solve(M, LD, n, rhs)) return false;
+    ++nsolve;
+    // scatter the solution back to parameter lanes
+    sm.pd[lane] = rhs;  // position-indexed
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const double zn = fr ? x + sm.pd[pos] : 0.0;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // first sign crossing among free delta coordinates along z -> zn
+    const bool viol = isd && fr && (zn * sgn_ < 0.0);
+    const double tt = viol ? ((z != zn) ? z / (z - zn) : 0.0) : 2.0;
+    double tmin = tt;
+    tmin = fmin(tmin, shfl_xor_f64<1>(tmin));
+    tmin = fmin(tmin, shfl_xor_f64<2>(tmin));
+    tmin = fmin(tmin, shfl_xor_f64<4>(tmin));
+    tmin = fmin(tmin, shfl_xor_f64<8>(tmin));
+    tmin = fmin(tmin, shfl_xor_f64<16>(tmin));
+    tmin = fmin(tmin, shfl_xor_f64<32>(tmin));
+    if (tmin < 2.0) {
+      const unsigned long long hit = __ballot(viol && tt == tmin);
+      const int jmin = __ffsll((long long)hit) - 1;
+      z = (lane < P) ? z + tmin * (zn - z) : 0.0;
+      if (lane == jmin) { z = 0.0; zero = true; sgn_ = 0.0; }
+      continue;
+    }
+    z = (lane < P) ? zn : 0.0;
+    // KKT of zero delta coordinates: |gh + H (z - x)| <= c
+    sm.pz[lane] = (lane < P) ? z - x : 0.0;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    double gq = 0.0;
+    const bool cand = isd && zero;
+    if (cand) {
+      double v = gh;
+      for (int q = 0; q < P; ++q) v += H[lane * LD + q] * sm.pz[q];
+      gq = v;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const double sc = (cand && fabs(gq) > c * (1.0 + 1e-12)) ? fabs(gq) : -1.0;
+    double smax = sc;
+    smax = fmax(smax, shfl_xor_f64<1>(smax));
+    smax = fmax(smax, shfl_xor_f64<2>(smax));
+    smax = fmax(smax, shfl_xor_f64<4>(smax));
+    smax = fmax(smax, shfl_xor_f64<8>(smax));
+    smax = fmax(smax, shfl_xor_f64<16>(smax));
+    smax = fmax(smax, shfl_xor_f64<32>(smax));
+    if (smax < 0.0) return true;
+    const unsigned long long hit = __ballot(sc == smax && sc >= 0.0);
+    const int jadd = __ffsll((long long)hit) - 1;
+    if (lane == jadd) { zero = false; sgn_ = -((gq > 0.0) - (gq < 0.0)); }
+  }
+  return true;
+}
+
+template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
+__device__ __forceinline__ void polish_run(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, double &x, double &f,
+                           double &g, int &n_eval, int &n_newton) {
+  const int lane = pf_lane(), wave = pf_wave();
+  const int S = a.S;
+  const double c = 1.0 / a.tau;
+  const bool isd = (lane >= 2 && lane < 2 + S);
+  double *ws = a.ws + (size_t)blockIdx.x * 3 * a.Tp;
+  n_newton = 0;
+  for (int it = 0; it < a.o.polish_max_iter; ++it) {
+    const double gh = isd ? g - c * (double)((x > 0.0) - (x < 0.0)) : g;
+    hessian_collective<NW, KMAX, O0, O1, O2, MODE>(a, sm, x, gh, ws);
+    if (wave == 0) {
+      double z;
+      int ns = 0;
+      const bool ok = qp_active<NW, KMAX, MODE>(a, sm, x, gh, c, z, ns);
+      const double d = (lane < a.P) ? z - x : 0.0;
+      double dec = wave_sum(gh * d);
+      const double l1 = wave_sum(isd ? fabs(z) - fabs(x) : 0.0);
+      dec += c * l1;
+      sm.pd[lane] = d;
+      if (lane == 0) { sm.fout[2] = ok ? dec : 0.0; sm.fout[3] = ok ? 1.0 : 0.0; }
+    }
+    __syncthreads();
+    const double dec = sm.fout[2];
+    const double d = sm.pd[lane];
+    __syncthreads();
+    if (!(dec < -1e-15 * fabs(f))) break;
+    ++n_newton;
+    double alpha = 1.0, fn = 0.0, gn = 0.0, xn = x;
+    bool acc = false;
+    for (int ls = 0; ls < 30; ++ls) {
+      xn = x + alpha * d;
+      const bool bad = eval_collective<NW, KMAX, O0, O1, O2, MODE>(a, sm, xn, fn, gn);
+      ++n_eval;
+      if (!bad && fn <= f + 1e-4 * alpha * dec) { acc = true; break; }
+      alpha *= 0.5;
+    }
+    if (!acc) break;
+    x = xn;
+    f = fn;
+    g = gn;
+  }
 }

@@ -61,12 +61,18 @@ for polish in (False, True):
     dt = time.time() - t0
     print(f"fit polish={polish}: {dt*1e3:.1f} ms  status={fit.status.cpu().numpy().tolist()}")
     print("   n_eval", fit.n_eval.cpu().numpy().tolist())
-    for s in range(min(n, 4)):
+    for s in range(min(n, 6)):
         st = po.build_problem(ds, Y[s])
-        th_o, f_o, st_o, it_o, ne_o = so.fit_setup(st)
-        print(f"   s{s}: gpu f={fit.f[s].item():.6f} f_stan={fit.f_stan[s].item():.6f} "
-              f"ne={fit.n_eval[s].item()} | oracle f={f_o:.6f} ne={ne_o} st={st_o} | "
-              f"rel={(fit.f[s].item()-f_o)/abs(f_o):+.2e}")
+        if polish:
+            th_o, f_o, st_o, it_o, ne_o, fst_o = so.fit_map(st)
+        else:
+            th_o, f_o, st_o, it_o, ne_o = so.fit_setup(st)
+        thg = fit.theta[s].cpu().numpy()
+        pt_g = po.predict_point(st, po.params_from_theta(thg, st.problem.S), ds)["yhat"]
+        pt_o = po.predict_point(st, po.params_from_theta(th_o, st.problem.S), ds)["yhat"]
+        print(f"   s{s}: gpu f={fit.f[s].item():.8f} f_stan={fit.f_stan[s].item():.6f} "
+              f"ne={fit.n_eval[s].item()} | oracle f={f_o:.8f} ne={ne_o} st={st_o} | "
+              f"rel={(fit.f[s].item()-f_o)/abs(f_o):+.2e} dyhat/ys={np.abs(pt_g-pt_o).max()/st.hist.y_scale:.1e}")
 
 fut = dfa.future_dates(ds, 90)
 fg = eng.predict_grid(fit, fut)

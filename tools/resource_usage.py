@@ -15,5 +15,5 @@ for line in out.splitlines():
         k, v = txt.split(":", 1); rows[cur][k.strip()] = v.strip()
 for n, r in rows.items():
     dm = subprocess.run(["llvm-cxxfilt", n], capture_output=True, text=True).stdout.strip() if False else n
-    print(f"{dm[:60]:60s} VGPR={r.get('VGPRs','?'):>4} AGPR={r.get('AGPRs','?'):>3} SGPR={r.get('SGPRs','?'):>4} "
+    print(f"{dm[:60]:60s} VGPR={r.get('VGPRs','?'):>4} AGPR={r.get('AGPRs','?'):>3} SGPR={r.get('SGPRs','?'):>4} LDS={r.get('LDS Size [bytes/block]','?'):>5} "
           f"spillV={r.get('VGPRs Spill','?'):>4} spillS={r.get('SGPRs Spill','?'):>4} scratch={r.get('ScratchSize [bytes/lane]','?'):>4} occ={r.get('Occupancy [waves/SIMD]','?')}")
