@@ -20,7 +20,8 @@ PF_ST_CONSTANT = 50
 # Every symbol include/prophet_hip.h declares (checked by tests/test_abi.py).
 EXPORTED = ["pf_ctx_create", "pf_ctx_destroy", "pf_last_error", "pf_default_fit_opts",
             "pf_num_changepoints", "pf_build_grid", "pf_prepare", "pf_objective_grad",
-            "pf_fit", "pf_predict"]
+            "pf_fit", "pf_predict", "pf_set_timing", "pf_read_timings", "pf_cv_metrics"]
+CV_METRICS = ["mse", "rmse", "mae", "mape", "smape", "coverage"]
 
 
 class EngineUnavailable(RuntimeError):
@@ -61,7 +62,19 @@ class PfPredictArgs(ctypes.Structure):
                 ("interval_width", ctypes.c_double), ("seed", ctypes.c_uint64),
                 ("yhat", vp), ("yhat_lower", vp), ("yhat_upper", vp),
                 ("trend", vp), ("trend_lower", vp), ("trend_upper", vp),
-                ("mult_terms", vp), ("add_terms", vp)]
+                ("mult_terms", vp), ("add_terms", vp),
+                ("n_comp", i32), ("comp_col0", i32 * 4), ("comp_ncol", i32 * 4), ("comp", vp),
+                ("series_id", vp)]
+
+
+class PfCvArgs(ctypes.Structure):
+    _fields_ = [("n_series", i32), ("n_rows", i32), ("n_groups", i32), ("window", i32),
+                ("group_start", vp), ("y", vp), ("yhat", vp), ("yhat_lower", vp),
+                ("yhat_upper", vp), ("metrics", vp)]
+
+
+class PfKernelTime(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char * 32), ("ms", ctypes.c_float), ("grid", i32)]
 
 
 _lib = None
@@ -97,6 +110,9 @@ def load(path: str = LIB_PATH):
     lib.pf_fit.argtypes = [vp, ctypes.POINTER(PfProblem), ctypes.POINTER(PfFitOpts),
                            vp, vp, vp, vp, vp, vp, vp]
     lib.pf_predict.argtypes = [vp, ctypes.POINTER(PfPredictArgs), vp]
+    lib.pf_cv_metrics.argtypes = [vp, ctypes.POINTER(PfCvArgs), vp]
+    lib.pf_set_timing.argtypes = [vp, ctypes.c_int]
+    lib.pf_read_timings.argtypes = [vp, ctypes.POINTER(PfKernelTime), ctypes.c_int]
     for name in EXPORTED:
         if name not in ("pf_default_fit_opts",):
             getattr(lib, name).restype = getattr(lib, name).restype or ctypes.c_int

@@ -1,0 +1,259 @@
+"""Batched fit / forecast of many series that share one date grid.
+
+The reference fits one Prophet per (store, item) group inside a Spark
+``applyInPandas`` call (notebooks/prophet/02_training.py:282-307).  Here the
+groups are packed into *buckets* — series whose non-NaN history dates and
+whose full date set (``history_dates``, NaN rows included) are identical —
+and each bucket is one dense ``Y[n, T_pad]`` float64 tensor in HBM, fitted
+and forecast by single kernel launches.
+
+Series identity: ``series_id(keys)`` = low 32 bits of splitmix64 of the packed
+(store, item) key.  It keys each series' Monte-Carlo RNG stream (so the
+intervals of a series do not depend on which bucket or GPU it landed on) and
+the GPU shard.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import engine as E
+
+NS_PER_DAY = E.NS_PER_DAY
+
+
+# ---------------------------------------------------------------------------
+# keys
+# ---------------------------------------------------------------------------
+def splitmix64(x: np.ndarray) -> np.ndarray:
+    """splitmix64 finaliser over uint64 (vectorised)."""
+    z = np.asarray(x, dtype=np.uint64).copy()
+    with np.errstate(over="ignore"):
+        z = z + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return z
+
+
+def pack_keys(keys: np.ndarray) -> np.ndarray:
+    """[n, k] integer keys -> uint64 (store << 32 | item for k == 2)."""
+    keys = np.asarray(keys)
+    if keys.ndim == 1:
+        keys = keys[:, None]
+    out = np.zeros(keys.shape[0], dtype=np.uint64)
+    for j in range(keys.shape[1]):
+        col = keys[:, j].astype(np.int64).astype(np.uint64) & np.uint64(0xFFFFFFFF)
+        out = (out << np.uint64(32)) | col if j else col
+    return out
+
+
+def series_hash(keys: np.ndarray) -> np.ndarray:
+    return splitmix64(pack_keys(keys))
+
+
+def series_id(keys: np.ndarray) -> np.ndarray:
+    """int32 RNG-stream key per series (bit pattern of the low 32 hash bits)."""
+    return (series_hash(keys) & np.uint64(0xFFFFFFFF)).astype(np.uint32).view(np.int32)
+
+
+def shard_of(keys: np.ndarray, world_size: int) -> np.ndarray:
+    """GPU shard of each series: splitmix64((store << 32) | item) mod G."""
+    return (series_hash(keys) % np.uint64(max(1, world_size))).astype(np.int64)
+
+
+# ---------------------------------------------------------------------------
+# grid helpers (UPSTREAM setup_dataframe / make_future_dataframe)
+# ---------------------------------------------------------------------------
+def to_ns(ds) -> np.ndarray:
+    """Any date-like column -> int64 nanoseconds since the epoch."""
+    import pandas as pd
+    arr = np.asarray(ds)
+    if arr.dtype.kind == "M":
+        return arr.astype("datetime64[ns]").astype(np.int64)
+    return pd.to_datetime(pd.Series(ds)).values.astype("datetime64[ns]").astype(np.int64)
+
+
+def future_dates(history_dates_ns: np.ndarray, periods: int, freq="D",
+                 include_history: bool = True) -> np.ndarray:
+    """UPSTREAM make_future_dataframe: ``periods`` dates after the last
+    history date at ``freq`` (pandas offset alias), optionally prefixed by the
+    history dates."""
+    import pandas as pd
+    h = np.unique(np.asarray(history_dates_ns, np.int64))
+    last = pd.Timestamp(int(h[-1]))
+    dates = pd.date_range(start=last, periods=periods + 1, freq=freq)
+    dates = dates[dates > last][:periods]
+    fut = dates.values.astype("datetime64[ns]").astype(np.int64)
+    return np.concatenate((h, fut)) if include_history else fut
+
+
+def min_positive_diff(ds_sorted: np.ndarray) -> int:
+    d = np.diff(ds_sorted)
+    d = d[d != 0]
+    return int(d.min()) if d.size else 0
+
+
+# ---------------------------------------------------------------------------
+# buckets
+# ---------------------------------------------------------------------------
+@dataclass
+class Bucket:
+    fit_ds: np.ndarray          # sorted non-NaN dates [T] (duplicates kept)
+    history_dates: np.ndarray   # sorted unique dates of all rows (NaN y included)
+    Y: np.ndarray               # [n, T] float64, columns aligned with fit_ds
+    members: np.ndarray         # positions in the caller's group list
+
+
+def bucket_groups(ds_list, y_list) -> list:
+    """Pack per-group (ds, y) arrays into buckets of identical grids.
+
+    Per group (UPSTREAM setup_dataframe): rows with NaN y are dropped from
+    the fit history but their dates stay in ``history_dates``; fewer than two
+    non-NaN rows is Prophet's ValueError."""
+    sig_to_bucket = {}
+    parts = []
+    for g, (ds, y) in enumerate(zip(ds_list, y_list)):
+        ds = np.asarray(ds, dtype=np.int64)
+        y = np.asarray(y, dtype=np.float64)
+        ok = ~np.isnan(y)
+        if int(ok.sum()) < 2:
+            raise ValueError("Dataframe has less than 2 non-NaN rows.")
+        order = np.argsort(ds[ok], kind="stable")
+        fds = ds[ok][order]
+        hd = np.unique(ds)
+        key = (fds.tobytes(), hd.tobytes())
+        b = sig_to_bucket.get(key)
+        if b is None:
+            b = len(parts)
+            sig_to_bucket[key] = b
+            parts.append((fds, hd, [], []))
+        parts[b][2].append(y[ok][order])
+        parts[b][3].append(g)
+    return [Bucket(fds, hd, np.stack(ys), np.asarray(mem, dtype=np.int64))
+            for fds, hd, ys, mem in parts]
+
+
+# ---------------------------------------------------------------------------
+# fitted batch
+# ---------------------------------------------------------------------------
+@dataclass
+class GridSpec:
+    """What a forecast needs from the fit grid (also what the params store
+    persists): seasonality spec, time scaling and the changepoints."""
+    seasons: list
+    start_ns: int
+    t_scale_ns: int
+    t_change: torch.Tensor
+
+
+class FittedBatch:
+    """n series fitted on one shared grid (all tensors on one GPU)."""
+
+    def __init__(self, engine: E.Engine, fit: E.FitResult, history_dates: np.ndarray,
+                 fit_ds: np.ndarray | None = None, series_ids: np.ndarray | None = None):
+        self.engine = engine
+        self.fit = fit
+        self.history_dates = np.asarray(history_dates, np.int64)
+        self.fit_ds = fit_ds
+        self.series_ids = None
+        if series_ids is not None:
+            self.series_ids = torch.from_numpy(np.ascontiguousarray(series_ids, dtype=np.int32)) \
+                .to(fit.theta.device)
+
+    @property
+    def n(self) -> int:
+        return int(self.fit.theta.shape[0])
+
+    @classmethod
+    def fit_dense(cls, engine: E.Engine, fit_ds: np.ndarray, Y, history_dates=None,
+                  series_ids=None, polish: bool = True, seasons=None) -> "FittedBatch":
+        """Fit every row of Y ([n, T] numpy or device tensor, raw y) on the
+        sorted date grid ``fit_ds`` (K1 grid + K2/K3 fit).  ``seasons``
+        overrides the auto rules (CV folds reuse the parent's seasonalities,
+        UPSTREAM diagnostics.prophet_copy)."""
+        cfg = engine.config
+        fit_ds = np.asarray(fit_ds, np.int64)
+        T = fit_ds.shape[0]
+        if T < 2:
+            raise ValueError("Dataframe has less than 2 non-NaN rows.")
+        start, t_scale = int(fit_ds[0]), int(fit_ds[-1] - fit_ds[0])
+        if t_scale <= 0:
+            raise ValueError("history must span more than one distinct date")
+        if seasons is None:
+            seasons = cfg.seasons(start, int(fit_ds[-1]), min_positive_diff(fit_ds))
+        grid = E.build_grid(fit_ds, seasons, start_ns=start, t_scale_ns=t_scale,
+                            n_changepoints=cfg.n_changepoints,
+                            changepoint_range=cfg.changepoint_range, device=engine.device)
+        dev = torch.device("cuda", engine.device)
+        n = int(Y.shape[0])
+        Yd = torch.zeros((n, grid.T_pad), dtype=torch.float64, device=dev)
+        if isinstance(Y, torch.Tensor):
+            Yd[:, :T] = Y[:, :T].to(dev, torch.float64)
+        else:
+            Yd[:, :T] = torch.from_numpy(np.ascontiguousarray(Y, dtype=np.float64)).to(dev)
+        fit = engine.fit(grid, Yd, polish=polish)
+        hd = fit_ds if history_dates is None else history_dates
+        return cls(engine, fit, np.unique(hd), fit_ds, series_ids)
+
+    def spec(self) -> GridSpec:
+        g = self.fit.grid
+        return GridSpec(list(g.seasons), int(g.start_ns), int(g.t_scale_ns), g.t_change)
+
+    def predict(self, ds_ns: np.ndarray, *, seed: int = 0, n_samples: int | None = None,
+                components: bool = True):
+        """Forecast every series of the batch on the dates ``ds_ns`` (sorted).
+        Returns (T, dict of float32 device tensors [n, T_pad])."""
+        ds_ns = np.asarray(ds_ns, np.int64)
+        fg = self.engine.predict_grid(self.fit, ds_ns)
+        out = self.engine.predict(self.fit, fg, n_samples=n_samples, seed=seed,
+                                  components=components, series_id=self.series_ids)
+        return fg.T, out
+
+    # -------------------------------------------------------- params store
+    def to_record(self, keys: np.ndarray | None = None) -> dict:
+        """Host arrays describing the fits (one params-store bucket)."""
+        g = self.fit.grid
+        rec = {
+            "theta": self.fit.theta.cpu().numpy(),
+            "y_scale": self.fit.y_scale.cpu().numpy(),
+            "f": self.fit.f.cpu().numpy(),
+            "status": self.fit.status.cpu().numpy(),
+            "n_eval": self.fit.n_eval.cpu().numpy(),
+            "t_change": g.t_change.cpu().numpy(),
+            "start_ns": np.int64(g.start_ns),
+            "t_scale_ns": np.int64(g.t_scale_ns),
+            "history_dates": self.history_dates,
+            "season_names": np.array([s[0] for s in g.seasons]),
+            "season_periods": np.array([s[1] for s in g.seasons], dtype=np.float64),
+            "season_orders": np.array([s[2] for s in g.seasons], dtype=np.int64),
+        }
+        if keys is not None:
+            rec["keys"] = np.asarray(keys, dtype=np.int64)
+        if self.series_ids is not None:
+            rec["series_id"] = self.series_ids.cpu().numpy()
+        return rec
+
+    @classmethod
+    def from_record(cls, engine: E.Engine, rec: dict, rows=None) -> "FittedBatch":
+        """Rebuild a (sub-)batch from a params-store record without refitting."""
+        dev = torch.device("cuda", engine.device)
+        sel = slice(None) if rows is None else np.asarray(rows)
+        theta = torch.from_numpy(np.ascontiguousarray(rec["theta"][sel])).to(dev)
+        n = theta.shape[0]
+        seasons = [(str(a), float(b), int(c)) for a, b, c in
+                   zip(rec["season_names"], rec["season_periods"], rec["season_orders"])]
+        spec = GridSpec(seasons, int(rec["start_ns"]), int(rec["t_scale_ns"]),
+                        torch.from_numpy(np.ascontiguousarray(rec["t_change"])).to(dev))
+
+        def _t(name, dtype):
+            return torch.from_numpy(np.ascontiguousarray(rec[name][sel]).astype(dtype)).to(dev)
+
+        fit = E.FitResult(spec, theta, _t("y_scale", np.float64), _t("f", np.float64),
+                          _t("f", np.float64), _t("status", np.int32),
+                          torch.zeros(n, dtype=torch.int32, device=dev), _t("n_eval", np.int32),
+                          engine.config)
+        sid = rec["series_id"][sel] if "series_id" in rec else None
+        return cls(engine, fit, rec["history_dates"], None, sid)

@@ -20,16 +20,30 @@
 
 #include "pf_common.h"
 #include "prophet_hip.h"
+#include "pf_cv.h"
 
 #ifndef M_PI
 #define M_PI 3.14159265358979323846
 #endif
+
+// Per-launch timing (pf_set_timing): a fixed pool of HIP event pairs recorded
+// on the launch stream around every kernel, read back by pf_read_timings.
+#define PF_MAX_TIMED 1024
+struct pf_timed {
+  const char *name;
+  hipEvent_t start, stop;
+  int grid;
+};
 
 struct pf_ctx {
   int device;
   char err[512];
   void *ws;         // scratch owned by the context (polish per-row scalars)
   size_t ws_bytes;
+  int timing;       // record events around launches
+  int n_timed;      // records since the last pf_read_timings
+  int n_events;     // event pairs created so far
+  pf_timed timed[PF_MAX_TIMED];
 };
 
 static char g_err_noctx[512] = "";
@@ -62,6 +76,31 @@ static int set_err(pf_ctx *ctx, const char *msg) {
       set_err(ctx, b_);                                                          \
       return -2;                                                                 \
     }                                                                            \
+  } while (0)
+
+// bracket a launch with the context's timing events (no-op unless enabled)
+static int timed_begin(pf_ctx *ctx, const char *name, int grid, hipStream_t st) {
+  if (!ctx || !ctx->timing || ctx->n_timed >= PF_MAX_TIMED) return -1;
+  const int i = ctx->n_timed;
+  if (i >= ctx->n_events) {
+    if (hipEventCreate(&ctx->timed[i].start) != hipSuccess) return -1;
+    if (hipEventCreate(&ctx->timed[i].stop) != hipSuccess) return -1;
+    ctx->n_events = i + 1;
+  }
+  ctx->timed[i].name = name;
+  ctx->timed[i].grid = grid;
+  if (hipEventRecord(ctx->timed[i].start, st) != hipSuccess) return -1;
+  ctx->n_timed = i + 1;
+  return i;
+}
+static void timed_end(pf_ctx *ctx, int i, hipStream_t st) {
+  if (i >= 0) (void)hipEventRecord(ctx->timed[i].stop, st);
+}
+#define PF_TIMED_LAUNCH(ctx, name, grid_n, st, ...)                              \
+  do {                                                                           \
+    const int ti_ = timed_begin(ctx, name, (int)(grid_n), st);                   \
+    hipLaunchKernelGGL(__VA_ARGS__);                                             \
+    timed_end(ctx, ti_, st);                                                     \
   } while (0)
 
 // ============================================================================
@@ -1176,6 +1215,10 @@ struct PredKArgs {
   float fr_lo, fr_hi;
   uint32_t seed0, seed1;
   float *yhat, *ylo, *yhi, *tr, *trlo, *trhi, *mult, *add;
+  int n_comp;
+  int comp_col0[4], comp_ncol[4];
+  float *comp;
+  const uint32_t *series_id;  // RNG stream key per series (NULL: batch index)
 };
 
 // k-th and (k+1)-th smallest of the wave's samples (v[q] = +inf if absent).
@@ -1242,7 +1285,7 @@ __device__ __forceinline__ float np_lerp(float a, float b, float t) {
 // trend offset of MC sample `smp` at time ti (in scaled units):
 // sum over the sample's new changepoints with ti >= t_c of delta_c (ti - t_c)
 __device__ __noinline__ double mc_trend_offset(uint32_t seed0, uint32_t seed1, double lam_pois,
-                                               double t_max, int series, int smp, double ti,
+                                               double t_max, uint32_t series, int smp, double ti,
                                                double lam) {
   const pf_u4 r0 = philox4x32_10(pf_u4{(uint32_t)smp, 0u, (uint32_t)series, 0x7EE2D00Du},
                                  seed0 ^ 0x5A5A5A5Au, seed1);
@@ -1278,6 +1321,7 @@ __global__ __launch_bounds__(256) void k_predict(PredKArgs a) {
   __shared__ float s_buf[4][64];
   __shared__ float s_off[4][64 * PF_NQ];
   const int series = blockIdx.y, lane = pf_lane(), wave = pf_wave();
+  const uint32_t sid = a.series_id ? a.series_id[series] : (uint32_t)series;
   const int P = a.P, S = a.S, K = a.K;
   if (wave == 0) {
     const double x = (lane < P) ? a.theta[(size_t)series * P + lane] : 0.0;
@@ -1321,6 +1365,18 @@ __global__ __launch_bounds__(256) void k_predict(PredKArgs a) {
       xbm = xv * s_bm[lane];
       xba = xv * s_ba[lane];
     }
+    if (a.comp) {
+      // per-block components: lanes of block b hold x*beta (mult or add part)
+      const double part = xbm + xba * ysc;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        if (b < a.n_comp) {
+          const bool inb = lane >= a.comp_col0[b] && lane < a.comp_col0[b] + a.comp_ncol[b];
+          const double cb = wave_sum(inb ? part : 0.0);
+          if (lane == 0) a.comp[((size_t)b * a.n_series + series) * a.Tp + row] = (float)cb;
+        }
+      }
+    }
     xbm = wave_sum(xbm);
     xba = wave_sum(xba);
     const double trs = linear ? (s_kseg[sg] * ti + s_mseg[sg]) : s_mseg[0];
@@ -1332,8 +1388,7 @@ __global__ __launch_bounds__(256) void k_predict(PredKArgs a) {
       float z[PF_NQ];
 #pragma unroll
       for (int c = 0; c < PF_NQ / 4; ++c) {
-        const pf_u4 rr = philox4x32_10(pf_u4{(uint32_t)c, (uint32_t)lane, (uint32_t)row,
-                                              (uint32_t)series},
+        const pf_u4 rr = philox4x32_10(pf_u4{(uint32_t)c, (uint32_t)lane, (uint32_t)row, sid},
                                        a.seed0, a.seed1);
         pf_box_muller(pf_u01f(rr.x), pf_u01f(rr.y), z[4 * c + 0], z[4 * c + 1]);
         pf_box_muller(pf_u01f(rr.z), pf_u01f(rr.w), z[4 * c + 2], z[4 * c + 3]);
@@ -1356,7 +1411,7 @@ __global__ __launch_bounds__(256) void k_predict(PredKArgs a) {
 #pragma unroll 1
         for (int q = 0; q < PF_NQ; ++q) {
           const int smp = lane + 64 * q;
-          offs[q * 64 + lane] = (smp < a.N) ? (float)(ysc * mc_trend_offset(a.seed0, a.seed1, a.lam_pois, a.t_max, series, smp, ti, lam)) : 0.0f;
+          offs[q * 64 + lane] = (smp < a.N) ? (float)(ysc * mc_trend_offset(a.seed0, a.seed1, a.lam_pois, a.t_max, sid, smp, ti, lam)) : 0.0f;
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -1418,6 +1473,9 @@ int pf_ctx_create(int device, pf_ctx **out) {
   c->err[0] = 0;
   c->ws = nullptr;
   c->ws_bytes = 0;
+  c->timing = 0;
+  c->n_timed = 0;
+  c->n_events = 0;
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess) {
     snprintf(g_err_noctx, sizeof g_err_noctx, "hipSetDevice(%d): %s", device, hipGetErrorString(e));
@@ -1439,7 +1497,34 @@ int pf_debug_stamps(unsigned long long *out, int reset) {
 }
 #endif
 
+int pf_set_timing(pf_ctx *ctx, int enable) {
+  if (!ctx) return set_err(nullptr, "pf_set_timing: NULL ctx");
+  ctx->timing = enable ? 1 : 0;
+  ctx->n_timed = 0;
+  return 0;
+}
+
+int pf_read_timings(pf_ctx *ctx, pf_kernel_time *out, int max_out) {
+  if (!ctx) return set_err(nullptr, "pf_read_timings: NULL ctx");
+  const int n = ctx->n_timed;
+  for (int i = 0; i < n && i < max_out; ++i) {
+    PF_HIP(ctx, hipEventSynchronize(ctx->timed[i].stop));
+    float ms = 0.f;
+    PF_HIP(ctx, hipEventElapsedTime(&ms, ctx->timed[i].start, ctx->timed[i].stop));
+    snprintf(out[i].name, sizeof out[i].name, "%s", ctx->timed[i].name);
+    out[i].ms = ms;
+    out[i].grid = ctx->timed[i].grid;
+  }
+  ctx->n_timed = 0;
+  return n < max_out ? n : max_out;
+}
+
 int pf_ctx_destroy(pf_ctx *ctx) {
+  if (ctx)
+    for (int i = 0; i < ctx->n_events; ++i) {
+      (void)hipEventDestroy(ctx->timed[i].start);
+      (void)hipEventDestroy(ctx->timed[i].stop);
+    }
   if (ctx && ctx->ws) (void)hipFree(ctx->ws);
   delete ctx;
   return 0;
@@ -1500,21 +1585,21 @@ int pf_build_grid(pf_ctx *ctx, const int64_t *ds_ns, int T, int T_pad, int64_t s
     ss.order[b] = seasons_host[b].order;
   }
   const int nb = (T_pad + 255) / 256;
-  hipLaunchKernelGGL(k_grid_features, dim3(nb), dim3(256), 0, st, ds_ns, T, T_pad, start_ns,
-                     t_scale_ns, ss, extra_cols, n_extra, t_out, XT_out);
+  PF_TIMED_LAUNCH(ctx, "k_grid_features", nb, st, k_grid_features, dim3(nb), dim3(256), 0, st,
+                  ds_ns, T, T_pad, start_ns, t_scale_ns, ss, extra_cols, n_extra, t_out, XT_out);
   PF_HIP(ctx, hipGetLastError());
   if (n_changepoints >= 0) {
     if (!cp_idx_out) return set_err(ctx, "pf_build_grid: cp_idx_out NULL");
     const int n_expect = pf_num_changepoints(T, n_changepoints, changepoint_range);
     if ((n_expect > 0 ? n_expect : 1) != S)
       return set_err(ctx, "pf_build_grid: S does not match pf_num_changepoints");
-    hipLaunchKernelGGL(k_grid_changepoints, dim3(1), dim3(64), 0, st, t_out, T, n_changepoints,
-                       changepoint_range, t_change_io, cp_idx_out);
+    PF_TIMED_LAUNCH(ctx, "k_grid_changepoints", 1, st, k_grid_changepoints, dim3(1), dim3(64), 0,
+                    st, t_out, T, n_changepoints, changepoint_range, t_change_io, cp_idx_out);
     PF_HIP(ctx, hipGetLastError());
   }
   const int ns = ((T_pad > S ? T_pad : S) + 255) / 256;
-  hipLaunchKernelGGL(k_grid_segments, dim3(ns), dim3(256), 0, st, t_out, T, T_pad, t_change_io, S,
-                     seg_out, cp_first_out);
+  PF_TIMED_LAUNCH(ctx, "k_grid_segments", ns, st, k_grid_segments, dim3(ns), dim3(256), 0, st,
+                  t_out, T, T_pad, t_change_io, S, seg_out, cp_first_out);
   PF_HIP(ctx, hipGetLastError());
   return 0;
 }
@@ -1529,9 +1614,9 @@ int pf_prepare(pf_ctx *ctx, int n_series, const pf_grid *grid, int growth, const
     return set_err(ctx, "pf_prepare: bad arguments");
   if (n_series == 0) return 0;
   const int P = 3 + grid->S + grid->K;
-  hipLaunchKernelGGL(k_prepare, dim3(n_series), dim3(256), 0, (hipStream_t)stream, grid->T,
-                     grid->T_pad, grid->t, growth, y, y_scale, y_scaled, theta0, status, P,
-                     grid->S);
+  PF_TIMED_LAUNCH(ctx, "k_prepare", n_series, (hipStream_t)stream, k_prepare, dim3(n_series),
+                  dim3(256), 0, (hipStream_t)stream, grid->T, grid->T_pad, grid->t, growth, y,
+                  y_scale, y_scaled, theta0, status, P, grid->S);
   PF_HIP(ctx, hipGetLastError());
   return 0;
 }
@@ -1571,19 +1656,19 @@ int launch_fitlike(pf_ctx *ctx, bool fit, const FitKArgs &a, int n, hipStream_t 
     auto kern = k_fit<NW, KMAX, O0, O1, O2, MODE>;
     PF_HIP(ctx, hipFuncSetAttribute((const void *)kern,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
-    hipLaunchKernelGGL(kern, dim3(n), dim3(NW * 64), smem, st, a);
+    PF_TIMED_LAUNCH(ctx, "k_fit", n, st, kern, dim3(n), dim3(NW * 64), smem, st, a);
     PF_HIP(ctx, hipGetLastError());
     if (a.o.polish && a.ws && a.growth == PF_GROWTH_LINEAR && a.K <= 32 && 2 + a.S <= 32) {
       auto kp = k_polish<NW, KMAX, O0, O1, O2, MODE>;
       PF_HIP(ctx, hipFuncSetAttribute((const void *)kp,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
-      hipLaunchKernelGGL(kp, dim3(n), dim3(NW * 64), smem, st, a);
+      PF_TIMED_LAUNCH(ctx, "k_polish", n, st, kp, dim3(n), dim3(NW * 64), smem, st, a);
     }
   } else {
     auto kern = k_objgrad<NW, KMAX, O0, O1, O2, MODE>;
     PF_HIP(ctx, hipFuncSetAttribute((const void *)kern,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
-    hipLaunchKernelGGL(kern, dim3(n), dim3(NW * 64), smem, st, a);
+    PF_TIMED_LAUNCH(ctx, "k_objgrad", n, st, kern, dim3(n), dim3(NW * 64), smem, st, a);
   }
   PF_HIP(ctx, hipGetLastError());
   return 0;
@@ -1711,6 +1796,14 @@ int pf_predict(pf_ctx *ctx, const pf_predict_args *p, void *stream) {
   a.trhi = p->trend_upper;
   a.mult = p->mult_terms;
   a.add = p->add_terms;
+  a.comp = p->comp;
+  a.series_id = p->series_id;
+  a.n_comp = p->comp ? p->n_comp : 0;
+  if (a.n_comp < 0 || a.n_comp > 4) return set_err(ctx, "pf_predict: n_comp must be in [0, 4]");
+  for (int b = 0; b < 4; ++b) {
+    a.comp_col0[b] = p->comp_col0[b];
+    a.comp_ncol[b] = p->comp_ncol[b];
+  }
   if (a.N > 0) {
     // percentile positions exactly as numpy: q = 100*(1 -/+ w)/2; idx = q/100*(n-1)
     const double lo_p = 100.0 * (1.0 - p->interval_width) / 2.0;
@@ -1730,7 +1823,35 @@ int pf_predict(pf_ctx *ctx, const pf_predict_args *p, void *stream) {
     if (a.N == 1) { a.k_lo = 0; a.fr_lo = 0.f; a.k_hi_neg = 0; a.fr_hi = 0.f; }
   }
   const dim3 grid((a.Tf + 15) / 16, a.n_series);
-  hipLaunchKernelGGL((k_predict<64, MODE_MIXED>), grid, dim3(256), 0, (hipStream_t)stream, a);
+  PF_TIMED_LAUNCH(ctx, "k_predict", grid.x * grid.y, (hipStream_t)stream,
+                  (k_predict<64, MODE_MIXED>), grid, dim3(256), 0, (hipStream_t)stream, a);
+  PF_HIP(ctx, hipGetLastError());
+  return 0;
+}
+
+int pf_cv_metrics(pf_ctx *ctx, const pf_cv_args *p, void *stream) {
+  if (!p) return set_err(ctx, "pf_cv_metrics: NULL args");
+  if (p->n_series < 0 || p->n_rows < 1 || p->n_groups < 1 || p->n_groups > PF_CV_GMAX ||
+      p->window < 1)
+    return set_err(ctx, "pf_cv_metrics: bad sizes (need n_rows >= 1, 1 <= n_groups <= 512, window >= 1)");
+  if (!p->group_start || !p->y || !p->yhat || !p->metrics)
+    return set_err(ctx, "pf_cv_metrics: NULL buffer");
+  if ((p->yhat_lower == nullptr) != (p->yhat_upper == nullptr))
+    return set_err(ctx, "pf_cv_metrics: yhat_lower/yhat_upper must be both set or both NULL");
+  if (p->n_series == 0) return 0;
+  CvKArgs a;
+  a.n_series = p->n_series;
+  a.n_rows = p->n_rows;
+  a.n_groups = p->n_groups;
+  a.window = p->window;
+  a.group_start = p->group_start;
+  a.y = p->y;
+  a.yhat = p->yhat;
+  a.ylo = p->yhat_lower;
+  a.yhi = p->yhat_upper;
+  a.metrics = p->metrics;
+  PF_TIMED_LAUNCH(ctx, "k_cv_metrics", p->n_series, (hipStream_t)stream, k_cv_metrics,
+                  dim3(p->n_series), dim3(64), 0, (hipStream_t)stream, a);
   PF_HIP(ctx, hipGetLastError());
   return 0;
 }

@@ -107,6 +107,18 @@ class Context:
         if rc != 0:
             raise RuntimeError(f"{what} failed ({rc}): {self.lib.pf_last_error(self.h).decode()}")
 
+    def set_timing(self, enable: bool):
+        self.check(self.lib.pf_set_timing(self.h, 1 if enable else 0), "pf_set_timing")
+
+    def read_timings(self):
+        """[(kernel name, ms, workgroups)] for launches since the last read
+        (HIP events recorded on each launch's stream; synchronises)."""
+        buf = (L.PfKernelTime * 1024)()
+        n = self.lib.pf_read_timings(self.h, buf, 1024)
+        if n < 0:
+            self.check(n, "pf_read_timings")
+        return [(buf[i].name.decode(), float(buf[i].ms), int(buf[i].grid)) for i in range(n)]
+
 
 def _stream(device) -> ctypes.c_void_p:
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
@@ -321,9 +333,12 @@ class Engine:
                           device=self.device)
 
     def predict(self, fit: FitResult, fgrid: DeviceGrid, n_samples: int | None = None,
-                seed: int = 0, components: bool = True) -> dict:
+                seed: int = 0, components: bool = True,
+                series_id: torch.Tensor | None = None) -> dict:
         """Point forecast + MC intervals for every fitted series on ``fgrid``.
-        Returns float32 device tensors [n, fgrid.T_pad] (valid columns :T)."""
+        Returns float32 device tensors [n, fgrid.T_pad] (valid columns :T).
+        ``series_id`` (int32/uint32 [n] on the device) keys each series' RNG
+        stream so the intervals do not depend on the batch composition."""
         n = fit.theta.shape[0]
         dev = fit.theta.device
         ns = self.config.uncertainty_samples if n_samples is None else n_samples
@@ -352,6 +367,21 @@ class Engine:
                                                      ("trend", "trend_lower", "trend_upper"))
             a.mult_terms = out["multiplicative_terms"].data_ptr()
             a.add_terms = out["additive_terms"].data_ptr()
+        if components and fgrid.seasons:
+            nb = min(4, len(fgrid.seasons))
+            comp = torch.empty((nb, n, fgrid.T_pad), dtype=torch.float32, device=dev)
+            col = 0
+            for b, (_, _, order) in enumerate(fgrid.seasons[:nb]):
+                a.comp_col0[b] = col
+                a.comp_ncol[b] = 2 * order
+                col += 2 * order
+            a.n_comp = nb
+            a.comp = comp.data_ptr()
+            for b, (name, _, _) in enumerate(fgrid.seasons[:nb]):
+                out[name] = comp[b]
+        if series_id is not None:
+            assert series_id.numel() == n and series_id.dtype == torch.int32 and series_id.is_cuda
+            a.series_id = series_id.data_ptr()
         rc = self.ctx.lib.pf_predict(self.ctx.h, ctypes.byref(a), _stream(self.device))
         self.ctx.check(rc, "pf_predict")
         return out

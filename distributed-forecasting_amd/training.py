@@ -1,0 +1,186 @@
+"""Drop-in training / forecasting functions of the reference notebooks.
+
+Reference (notebooks/prophet/02_training.py):
+  train_model(history_pd, store=None) -> Prophet            :150-198
+  make_prediction(model) -> DataFrame                        :201-205
+  forecast_item(history_pd) -> DataFrame                     :208-223
+  forecast_store_item(history_pd) -> DataFrame               :282-301
+The per-group functions keep their signatures (Spark ``applyInPandas`` can
+call them unchanged; each is a batch of one).  ``forecast_store_items`` is
+the batched entry: it returns the rows that
+``groupBy('store','item').applyInPandas(forecast_store_item, schema)`` would
+(:305-307), computed bucket-by-bucket on the GPU.
+
+Output assembly follows the reference exactly (row a9 of SURVEY.md §8):
+``y`` is copied *by index position* from the incoming group frame (NaN past
+its length), keys are broadcast from the group's first row, and the columns
+are ``[ds, store, item, y, yhat, yhat_upper, yhat_lower]`` cast to the Spark
+schema (keys int32, values float32, ds datetime64[ns] at midnight).
+"""
+from __future__ import annotations
+
+import numpy as np
+import pandas as pd
+
+from . import batch as B
+from . import engine as E
+from .forecaster import SIMPLE_ATTRIBUTES, Prophet, get_engine
+
+HORIZON_DAYS = 90
+SCHEMA_STORE_ITEM = ["ds", "store", "item", "y", "yhat", "yhat_upper", "yhat_lower"]
+SCHEMA_ITEM = ["ds", "item", "y", "yhat", "yhat_upper", "yhat_lower"]
+
+
+def reference_model(**over) -> Prophet:
+    """The constructor call of 02_training.py:162-169."""
+    kw = dict(interval_width=0.95, growth="linear", daily_seasonality=False,
+              weekly_seasonality=True, yearly_seasonality=True,
+              seasonality_mode="multiplicative")
+    kw.update(over)
+    return Prophet(**kw)
+
+
+def extract_params(pr_model: Prophet) -> dict:
+    """02_training.py:146-147 (serialize.SIMPLE_ATTRIBUTES)."""
+    return {attr: getattr(pr_model, attr) for attr in SIMPLE_ATTRIBUTES}
+
+
+# ---------------------------------------------------------------------------
+# per-group API (batch of one)
+# ---------------------------------------------------------------------------
+def train_model(history_pd: pd.DataFrame, store: int = None, *, params_store=None,
+                cv_metrics: bool = False, device=None) -> Prophet:
+    """02_training.py:150-198 without MLflow: fit the reference model.
+
+    ``params_store`` (a ``ParamsStore``) receives the fitted parameters (the
+    reference logs params + model artifact to MLflow, :190-196).  With
+    ``cv_metrics`` the reference's cross-validation metrics (:178-188) are
+    computed and attached as ``model.metrics``."""
+    model = reference_model(device=device)
+    model.fit(history_pd)
+    item = history_pd["item"].iloc[0]
+    model.run_name = f"run_item_{item}_store_{store if store else 'all'}"
+    if cv_metrics:
+        from .diagnostics import cv_metrics_batch
+        fds = B.to_ns(model.history["ds"])
+        y = model.history["y"].to_numpy(np.float64)
+        model.metrics = {k: float(v[0]) for k, v in
+                         cv_metrics_batch(model._batch.engine, fds, y[None, :]).items()}
+    if params_store is not None:
+        key = (int(store) if store else -1, int(item))
+        params_store.put_batch(model._batch, np.array([key], dtype=np.int64))
+    return model
+
+
+def make_prediction(model: Prophet) -> pd.DataFrame:
+    """02_training.py:201-205."""
+    future_pd = model.make_future_dataframe(periods=HORIZON_DAYS, freq="d",
+                                            include_history=True)
+    return model.predict(future_pd)
+
+
+def _assemble_one(history_pd, forecast_pd, key_cols):
+    out = pd.DataFrame({"ds": forecast_pd["ds"].values})
+    yin = history_pd["y"].to_numpy(np.float64)
+    y = np.full(len(out), np.nan)
+    m = min(len(out), len(yin))
+    y[:m] = yin[:m]                       # forecast_pd['y'] = history_pd['y'] (by position)
+    for k in key_cols:
+        out[k] = np.int32(history_pd[k].iloc[0])
+    out["y"] = y.astype(np.float32)
+    for k in ("yhat", "yhat_upper", "yhat_lower"):
+        out[k] = forecast_pd[k].to_numpy(np.float32)
+    return out
+
+
+def forecast_item(history_pd: pd.DataFrame) -> pd.DataFrame:
+    """02_training.py:208-223 (item-level, schema of :233)."""
+    model = train_model(history_pd)
+    forecast_pd = make_prediction(model)
+    return _assemble_one(history_pd.reset_index(drop=True), forecast_pd, ["item"])[SCHEMA_ITEM]
+
+
+def forecast_store_item(history_pd: pd.DataFrame) -> pd.DataFrame:
+    """02_training.py:282-301 (schema of :307)."""
+    store = history_pd["store"].iloc[0]
+    model = train_model(history_pd, store=store)
+    forecast_pd = make_prediction(model)
+    return _assemble_one(history_pd.reset_index(drop=True), forecast_pd,
+                         ["store", "item"])[SCHEMA_STORE_ITEM]
+
+
+# ---------------------------------------------------------------------------
+# batched API
+# ---------------------------------------------------------------------------
+def group_frame(df: pd.DataFrame, keys):
+    """Split a long frame into groups (original row order kept inside each
+    group, like the frames applyInPandas hands to the UDF).
+    Returns (group keys [G, k] int64, list of row-position arrays)."""
+    kv = np.stack([df[k].to_numpy(np.int64) for k in keys], axis=1)
+    order = np.lexsort(kv.T[::-1])                  # stable: keeps row order in a group
+    sk = kv[order]
+    brk = np.flatnonzero(np.any(sk[1:] != sk[:-1], axis=1)) + 1
+    starts = np.concatenate(([0], brk))
+    ends = np.concatenate((brk, [len(order)]))
+    return sk[starts], [order[s:e] for s, e in zip(starts, ends)]
+
+
+def forecast_store_items(df: pd.DataFrame, keys=("store", "item"), *, periods: int = HORIZON_DAYS,
+                         freq="d", config: E.ProphetConfig | None = None, device=None,
+                         seed: int = 0, params_store=None, rank: int = 0,
+                         world_size: int = 1, return_fits: bool = False):
+    """Batched equivalent of
+    ``df.groupBy(*keys).applyInPandas(forecast_store_item, schema)``.
+
+    With ``world_size > 1`` only the groups whose splitmix64 key hash maps to
+    ``rank`` are processed; ``parallel.gather_frames``
+    collects the per-rank frames."""
+    keys = list(keys)
+    cfg = config or E.ProphetConfig.reference()
+    eng = get_engine(cfg, device)
+    gkeys, rows = group_frame(df, keys)
+    if world_size > 1:
+        mine = np.flatnonzero(B.shard_of(gkeys, world_size) == rank)
+        gkeys = gkeys[mine]
+        rows = [rows[i] for i in mine]
+    ds_all = B.to_ns(df["ds"])
+    y_all = df["y"].to_numpy(np.float64)
+    ds_list = [ds_all[r] for r in rows]
+    y_list = [y_all[r] for r in rows]
+    buckets = B.bucket_groups(ds_list, y_list)
+    frames, fits = [], []
+    for bk in buckets:
+        bkeys = gkeys[bk.members]
+        fb = B.FittedBatch.fit_dense(eng, bk.fit_ds, bk.Y, history_dates=bk.history_dates,
+                                     series_ids=B.series_id(bkeys))
+        fut = B.future_dates(bk.history_dates, periods, freq, include_history=True)
+        Tf, out = fb.predict(fut, seed=seed, components=False)
+        host = {k: out[k][:, :Tf].cpu().numpy() for k in ("yhat", "yhat_upper", "yhat_lower")}
+        n = len(bk.members)
+        yin = np.full((n, Tf), np.nan)
+        for i, g in enumerate(bk.members):
+            v = y_list[g]
+            m = min(Tf, len(v))
+            yin[i, :m] = v[:m]
+        fr = {"ds": np.tile(fut.astype("datetime64[ns]"), n)}
+        for j, k in enumerate(keys):
+            fr[k] = np.repeat(bkeys[:, j], Tf).astype(np.int32)
+        fr["y"] = yin.reshape(-1).astype(np.float32)
+        for k in ("yhat", "yhat_upper", "yhat_lower"):
+            fr[k] = host[k].reshape(-1).astype(np.float32)
+        frames.append(pd.DataFrame(fr))
+        if params_store is not None:
+            params_store.put_batch(fb, bkeys)
+        if return_fits:
+            fits.append((bkeys, fb))
+    cols = ["ds"] + keys + ["y", "yhat", "yhat_upper", "yhat_lower"]
+    res = (pd.concat(frames, ignore_index=True) if frames else
+           pd.DataFrame({c: pd.Series(dtype=("datetime64[ns]" if c == "ds" else
+                                              np.int32 if c in keys else np.float32))
+                         for c in cols}))[cols]
+    return (res, fits) if return_fits else res
+
+
+def forecast_items(df: pd.DataFrame, **kw):
+    """Batched ``groupBy('item').applyInPandas(forecast_item, ...)`` (:232-233)."""
+    return forecast_store_items(df, keys=("item",), **kw)

@@ -97,6 +97,18 @@ int pf_ctx_destroy(pf_ctx *ctx);
 const char *pf_last_error(pf_ctx *ctx);
 void pf_default_fit_opts(pf_fit_opts *o);
 
+/* Per-kernel timing (measurement only; no reference counterpart).  When
+ * enabled, every launch is bracketed by HIP events on its own stream;
+ * pf_read_timings synchronises on them, returns the number of records
+ * written (<= max_out, at most 1024 per read) and clears the list.         */
+typedef struct {
+  char name[32];
+  float ms;
+  int32_t grid;   /* workgroups launched */
+} pf_kernel_time;
+int pf_set_timing(pf_ctx *ctx, int enable);
+int pf_read_timings(pf_ctx *ctx, pf_kernel_time *out, int max_out);
+
 /* Host-side helper (no GPU): number of changepoints Prophet will place for a
  * history of T rows (set_changepoints clamp: n_cp+1 > floor(T*range) → floor-1). */
 int pf_num_changepoints(int T, int n_changepoints, double changepoint_range);
@@ -157,9 +169,38 @@ typedef struct {
   float *yhat, *yhat_lower, *yhat_upper;
   float *trend, *trend_lower, *trend_upper;
   float *mult_terms, *add_terms;
+  /* optional per-seasonality components (Prophet's 'yearly', 'weekly', ...):
+   * block b covers columns [comp_col0[b], comp_col0[b]+comp_ncol[b]); output
+   * comp[(b*n + s)*T_pad + row] (additive blocks already x y_scale).      */
+  int32_t n_comp;
+  int32_t comp_col0[4], comp_ncol[4];
+  float *comp;
+  /* optional [n_series] RNG stream key per series (e.g. a hash of
+   * (store, item)) so samples do not depend on batch position; NULL: use
+   * the batch index.                                                      */
+  const uint32_t *series_id;
 } pf_predict_args;
 
 int pf_predict(pf_ctx *ctx, const pf_predict_args *args, void *stream);
+
+/* ------------------------------------------ K6: cross-validation metrics
+ * Replaces UPSTREAM diagnostics.performance_metrics(df_cv, rolling_window=0.1)
+ * followed by the notebook's mean over horizons (02_training.py:178-188):
+ * per series, rolling_mean_by_h over the CV rows with window w, then the mean
+ * of the rolled values.  Rows (the concatenated fold predictions) must be
+ * sorted by horizon; group_start[n_groups+1] delimits equal-horizon runs and
+ * is shared by all series.  MAPE is NaN when min|y| < 1e-8 (UPSTREAM skips
+ * it); coverage is NaN when yhat_lower/upper are NULL.                    */
+enum { PF_CV_MSE = 0, PF_CV_RMSE = 1, PF_CV_MAE = 2, PF_CV_MAPE = 3, PF_CV_SMAPE = 4,
+       PF_CV_COVERAGE = 5, PF_CV_NMETRICS = 6 };
+typedef struct {
+  int32_t n_series, n_rows, n_groups, window;
+  const int32_t *group_start;          /* [n_groups + 1], n_groups <= 512 */
+  const double *y;                     /* [n_series, n_rows] actuals       */
+  const float *yhat, *yhat_lower, *yhat_upper;   /* [n_series, n_rows]     */
+  double *metrics;                     /* [n_series, PF_CV_NMETRICS]       */
+} pf_cv_args;
+int pf_cv_metrics(pf_ctx *ctx, const pf_cv_args *args, void *stream);
 
 #ifdef __cplusplus
 }

@@ -606,12 +606,16 @@ def rolling_mean_by_h(x, h, w):
 
 
 def performance_metrics(y, yhat, horizon, rolling_window=0.1,
-                        metrics=("mse", "rmse", "mae", "mape")):
+                        metrics=("mse", "rmse", "mae", "mape"), yhat_lower=None,
+                        yhat_upper=None):
     """Rolling-by-horizon means as in UPSTREAM performance_metrics; MAPE is
     skipped when min|y| < 1e-8.  Returns dict metric -> per-horizon array."""
     y, yhat, horizon = map(np.asarray, (y, yhat, horizon))
     order = np.argsort(horizon, kind="stable")
     y, yhat, horizon = y[order], yhat[order], horizon[order]
+    if yhat_lower is not None:
+        yhat_lower = np.asarray(yhat_lower)[order]
+        yhat_upper = np.asarray(yhat_upper)[order]
     n = len(y)
     w = int(rolling_window * n)
     w = max(w, 1)
@@ -631,4 +635,35 @@ def performance_metrics(y, yhat, horizon, rolling_window=0.1,
     if "mape" in metrics and not (np.abs(y).min() < 1e-8):
         hs, v = rolling_mean_by_h(np.abs((y - yhat) / y), horizon, w)
         out["mape"] = v
+    if "smape" in metrics:
+        sape = 2 * np.abs(yhat - y) / (np.abs(y) + np.abs(yhat))
+        hs, v = rolling_mean_by_h(sape, horizon, w)
+        out["smape"] = v
+    if "coverage" in metrics and yhat_lower is not None:
+        cov = ((y >= yhat_lower) & (y <= yhat_upper)).astype(np.float64)
+        hs, v = rolling_mean_by_h(cov, horizon, w)
+        out["coverage"] = v
     return out
+
+
+def cv_metric_means(ds_ns, y, horizon_days=90, period_days=360, initial_days=730, cfg=None,
+                    fit=None, metrics=("mse", "rmse", "mae", "mape", "smape")):
+    """02_training.py:178-188 end to end on the CPU: cutoffs, one refit per
+    fold (``fit(setup) -> theta``), point forecast of the fold's horizon,
+    performance_metrics, mean over horizons.  Returns dict metric -> float
+    (NaN where UPSTREAM skips the metric)."""
+    ds_ns = np.asarray(ds_ns, np.int64)
+    y = np.asarray(y, np.float64)
+    H = int(horizon_days * NS_PER_DAY)
+    cut = generate_cutoffs(ds_ns, H, int(initial_days * NS_PER_DAY), int(period_days * NS_PER_DAY))
+    ys, fs, hs = [], [], []
+    for c in cut:
+        tr = ds_ns <= c
+        te = (ds_ns > c) & (ds_ns <= c + H)
+        st = build_problem(ds_ns[tr], y[tr], cfg)
+        th = fit(st)
+        pt = predict_point(st, params_from_theta(th, st.problem.S), ds_ns[te], cfg)
+        ys.append(y[te]); fs.append(pt["yhat"]); hs.append(ds_ns[te] - c)
+    pm = performance_metrics(np.concatenate(ys), np.concatenate(fs), np.concatenate(hs),
+                             metrics=metrics)
+    return {m: (float(np.mean(pm[m])) if m in pm else float("nan")) for m in metrics}

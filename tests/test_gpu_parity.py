@@ -1,0 +1,394 @@
+"""GPU parity: the HIP kernels (through the C ABI) against the CPU oracle and
+the committed golden fixtures.  Tolerances (BASELINE.json north_star):
+  * grid indexing / changepoints: bit-exact;
+  * fitted objective no worse than the oracle's Stan-faithful optimum + 1e-6 rel;
+  * point forecast max|Δyhat| / y_scale <= 1e-3 (we also check the polished
+    MAP to 1e-6, which the exact-MAP polish reaches);
+  * intervals within Monte-Carlo error of the oracle's sampler.
+"""
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+import distributed_forecasting_amd as dfa
+from distributed_forecasting_amd import batch as B, synthetic
+from distributed_forecasting_amd.engine import NS_PER_DAY
+from oracle import prophet_oracle as po
+from oracle import stan_oracle as so
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    return dfa.Engine(0)
+
+
+def _grid(eng, ds, seasons=None):
+    seasons = seasons or eng.config.seasons(int(ds[0]), int(ds[-1]), int(ds[1] - ds[0]))
+    return dfa.build_grid(ds, seasons, start_ns=int(ds[0]), t_scale_ns=int(ds[-1] - ds[0]))
+
+
+def _Y(grid, Y):
+    Yd = torch.zeros((Y.shape[0], grid.T_pad), dtype=torch.float64, device="cuda")
+    Yd[:, :grid.T] = torch.from_numpy(Y).cuda()
+    return Yd
+
+
+# ----------------------------------------------------------------- K1 grid
+@pytest.mark.parametrize("span", [("2013-01-01", "2017-12-31"), ("2016-01-01", "2017-12-30"),
+                                  ("2013-01-01", "2015-10-13"), ("2017-01-01", "2017-01-10")])
+def test_grid_bit_exact(eng, span):
+    ds = synthetic.daily_dates(*span)
+    g = _grid(eng, ds)
+    h = po.setup_history(ds, np.ones(len(ds)))
+    assert np.array_equal(g.t[:g.T].cpu().numpy(), h.t)
+    cp = po.changepoint_indices(len(ds))
+    if len(cp):
+        assert g.cp_idx.cpu().numpy()[:len(cp)].tolist() == cp.tolist()
+        assert np.array_equal(g.t_change.cpu().numpy(), h.t[cp])
+    X = po.make_features(ds)[0]
+    XT = g.XT.view(g.K, g.T_pad)[:, :g.T].cpu().numpy()
+    assert np.max(np.abs(XT.T - X)) < 1e-13
+    tc = g.t_change.cpu().numpy()
+    seg = g.seg[:g.T].cpu().numpy()
+    assert np.array_equal(seg, (h.t[:, None] >= tc[None, :]).sum(1))
+
+
+def test_grid_irregular_dates(eng):
+    ds = synthetic.daily_dates()
+    keep = np.ones(len(ds), bool)
+    keep[np.random.default_rng(3).choice(len(ds), 300, replace=False)] = False
+    ds = ds[keep]
+    g = _grid(eng, ds, [("yearly", 365.25, 10), ("weekly", 7.0, 3)])
+    h = po.setup_history(ds, np.ones(len(ds)))
+    assert np.array_equal(g.t[:g.T].cpu().numpy(), h.t)
+    cp = po.changepoint_indices(len(ds))
+    assert g.cp_idx.cpu().numpy().tolist() == cp.tolist()
+
+
+# --------------------------------------------------------- K2 objective/grad
+def test_objective_gradient(eng, golden_ref):
+    ds, Y = golden_ref["ds_ns"], golden_ref["Y"]
+    g = _grid(eng, ds)
+    _, ys, th0, _ = eng.prepare(g, _Y(g, Y))
+    assert np.array_equal(th0.cpu().numpy(), golden_ref["theta0"])
+    rng = np.random.default_rng(0)
+    th = golden_ref["theta0"].copy()
+    S = 25
+    th[:, 2:2 + S] = rng.normal(0, 0.02, (8, S))
+    th[:, 3 + S:] = rng.normal(0, 0.05, (8, 26))
+    th[:, 2 + S] = -1.5
+    f, gr = eng.objective_grad(g, ys, torch.from_numpy(th).cuda())
+    f, gr = f.cpu().numpy(), gr.cpu().numpy()
+    for s in range(8):
+        pb = po.build_problem(ds, Y[s]).problem
+        fo, go, _ = so.objective(pb, th[s])
+        assert abs(f[s] - fo) <= 1e-12 * abs(fo)
+        assert np.max(np.abs(gr[s] - go)) <= 1e-11 * np.max(np.abs(go))
+
+
+# ----------------------------------------------------------------- K3 fit
+def test_fit_objective_and_yhat(eng, golden_ref):
+    ds, Y, fut = golden_ref["ds_ns"], golden_ref["Y"], golden_ref["fut_ns"]
+    g = _grid(eng, ds)
+    fit = eng.fit(g, _Y(g, Y))
+    f = fit.f.cpu().numpy()
+    st = fit.status.cpu().numpy()
+    assert np.all(np.isin(st, [0, 10, 20, 21, 30, 31]))
+    # objective no worse than the oracle's Stan-faithful optimum (+1e-6 rel)
+    assert np.all(f <= golden_ref["f_stan"] + 1e-6 * np.abs(golden_ref["f_stan"]))
+    # and equal to the oracle's polished MAP
+    assert np.all(np.abs(f - golden_ref["f_map"]) <= 1e-9 * np.abs(golden_ref["f_map"]))
+    fg = eng.predict_grid(fit, fut)
+    out = eng.predict(fit, fg, seed=5)
+    yh = out["yhat"][:, :fg.T].cpu().numpy()
+    ysc = np.abs(Y).max(1)
+    err = np.max(np.abs(yh - golden_ref["yhat"]), axis=1) / ysc
+    assert np.all(err <= 1e-3)          # north-star bar
+    assert np.all(err <= 1e-6)          # what the exact MAP + fp32 output reaches
+    tr = out["trend"][:, :fg.T].cpu().numpy()
+    assert np.max(np.abs(tr - golden_ref["trend"]) / ysc[:, None]) <= 1e-6
+
+
+def test_fit_many_vs_stan_phase(eng):
+    """64 fresh series: objective no worse than the oracle's Stan L-BFGS."""
+    ds = synthetic.daily_dates()
+    Y = synthetic.sales_matrix(64, ds, seed=99)
+    g = _grid(eng, ds)
+    fit = eng.fit(g, _Y(g, Y))
+    f = fit.f.cpu().numpy()
+    for s in range(0, 64, 4):
+        setup = po.build_problem(ds, Y[s])
+        _, f_o, *_ = so.fit_setup(setup)
+        assert f[s] <= f_o + 1e-6 * abs(f_o)
+
+
+def test_fit_without_polish_is_stan_faithful(eng, golden_ref):
+    """Stan phase only: same stopping rules, so the objective is within the
+    stall band of the oracle's Stan run (1e-4 rel) and never above f0."""
+    ds, Y = golden_ref["ds_ns"], golden_ref["Y"]
+    g = _grid(eng, ds)
+    fit = eng.fit(g, _Y(g, Y), polish=False)
+    f = fit.f.cpu().numpy()
+    assert np.all(np.abs(f - golden_ref["f_stan"]) <= 1e-4 * np.abs(golden_ref["f_stan"]))
+    assert np.all(np.isin(fit.status.cpu().numpy(), [0, 10, 20, 21, 30, 31]))
+
+
+# --------------------------------------------------------- K5 intervals
+def test_intervals_within_mc_error(eng, golden_ref):
+    ds, Y, fut = golden_ref["ds_ns"], golden_ref["Y"], golden_ref["fut_ns"]
+    g = _grid(eng, ds)
+    fit = eng.fit(g, _Y(g, Y))
+    fg = eng.predict_grid(fit, fut)
+    out = eng.predict(fit, fg, seed=11)
+    ysc = np.abs(Y).max(1)
+    for s in range(8):
+        sd = np.exp(golden_ref["theta_map"][s, 27]) * ysc[s]
+        for k in ("yhat_lower", "yhat_upper"):
+            d = (out[k][s, :fg.T].cpu().numpy() - golden_ref[k][s]) / sd
+            # two independent 1000-sample estimates of a 2.5%/97.5% quantile
+            # differ by ~0.12 sd (1 s.e.); over ~1900 rows the max is ~4 s.e.
+            assert abs(d.mean()) < 0.03
+            assert np.mean(np.abs(d)) < 0.15
+            assert np.max(np.abs(d)) < 0.8
+        # future trend band: widens past the history, like the oracle's
+        tlo = out["trend_lower"][s, :fg.T].cpu().numpy()
+        thi = out["trend_upper"][s, :fg.T].cpu().numpy()
+        w_g = thi[-1] - tlo[-1]
+        w_o = golden_ref["trend_upper"][s, -1] - golden_ref["trend_lower"][s, -1]
+        assert 0.5 * w_o < w_g < 2.0 * w_o
+        assert np.allclose(tlo[:1826], thi[:1826], rtol=0, atol=1e-4 * ysc[s])
+
+
+def test_interval_coverage_history(eng, golden_ref):
+    ds, Y = golden_ref["ds_ns"], golden_ref["Y"]
+    g = _grid(eng, ds)
+    fit = eng.fit(g, _Y(g, Y))
+    out = eng.predict(fit, eng.predict_grid(fit, ds), seed=3)
+    lo = out["yhat_lower"][:, :len(ds)].cpu().numpy()
+    hi = out["yhat_upper"][:, :len(ds)].cpu().numpy()
+    cov = np.mean((Y >= lo) & (Y <= hi))
+    assert 0.90 < cov < 0.98
+
+
+def test_predict_seed_and_series_id(eng, golden_ref):
+    ds, Y, fut = golden_ref["ds_ns"], golden_ref["Y"], golden_ref["fut_ns"]
+    g = _grid(eng, ds)
+    fit = eng.fit(g, _Y(g, Y))
+    fg = eng.predict_grid(fit, fut)
+    sid = torch.arange(100, 108, dtype=torch.int32, device="cuda")
+    a = eng.predict(fit, fg, seed=1, series_id=sid)["yhat_lower"].cpu()
+    b = eng.predict(fit, fg, seed=1, series_id=sid)["yhat_lower"].cpu()
+    c = eng.predict(fit, fg, seed=2, series_id=sid)["yhat_lower"].cpu()
+    assert torch.equal(a, b) and not torch.equal(a, c)
+
+
+# --------------------------------------------------------------- edge cases
+def test_constant_series(eng):
+    ds = synthetic.daily_dates()
+    Y = np.stack([np.full(len(ds), 7.0), np.zeros(len(ds))])
+    g = _grid(eng, ds)
+    fit = eng.fit(g, _Y(g, Y))
+    assert fit.status.cpu().tolist() == [50, 50]
+    th = fit.theta.cpu().numpy()
+    assert np.allclose(np.exp(th[:, 27]), 1e-9, rtol=1e-12)
+    out = eng.predict(fit, eng.predict_grid(fit, B.future_dates(ds, 90)))
+    yh = out["yhat"][:, :1916].cpu().numpy()
+    assert np.allclose(yh[0], 7.0, atol=1e-5) and np.allclose(yh[1], 0.0, atol=1e-6)
+    assert np.allclose(out["yhat_lower"][0, :1826].cpu().numpy(), 7.0, atol=1e-4)
+
+
+def test_noise_free_linear(eng, golden_edge):
+    ds = synthetic.daily_dates()
+    y = golden_edge["lin_y"][None, :]
+    g = _grid(eng, ds)
+    fit = eng.fit(g, _Y(g, y))
+    fg = eng.predict_grid(fit, B.future_dates(ds, 90))
+    yh = eng.predict(fit, fg)["yhat"][0, :fg.T].cpu().numpy()
+    assert np.max(np.abs(yh - golden_edge["lin_yhat"])) / y.max() < 1e-5
+    assert np.max(np.abs(yh[:1826] - y[0])) / y.max() < 1e-3
+
+
+def test_short_series_weekly_only(eng, golden_edge):
+    ds = golden_edge["short_ds"]
+    y = golden_edge["short_y"][None, :]
+    cfg = dfa.ProphetConfig.reference()
+    cfg.yearly_seasonality = "auto"
+    e2 = dfa.Engine(0, cfg)
+    seasons = cfg.seasons(int(ds[0]), int(ds[-1]), NS_PER_DAY)
+    assert [s[0] for s in seasons] == ["weekly"]
+    g = _grid(e2, ds, seasons)
+    assert g.cp_idx.cpu().numpy().tolist() == golden_edge["short_cp_idx"].tolist()
+    fit = e2.fit(g, _Y(g, y))
+    f = fit.f.cpu().numpy()[0]
+    assert f <= golden_edge["short_f"] + 1e-6 * abs(golden_edge["short_f"])
+    fg = e2.predict_grid(fit, B.future_dates(ds, 90))
+    yh = e2.predict(fit, fg)["yhat"][0, :fg.T].cpu().numpy()
+    assert np.max(np.abs(yh - golden_edge["short_yhat"])) / np.abs(y).max() < 1e-4
+
+
+def test_730_day_grid(eng, golden_edge):
+    ds = golden_edge["d730_ds"]
+    Y = golden_edge["d730_y"]
+    g = _grid(eng, ds)
+    assert g.cp_idx.cpu().numpy().tolist() == golden_edge["d730_cp_idx"].tolist()
+    fit = eng.fit(g, _Y(g, Y))
+    f = fit.f.cpu().numpy()
+    assert np.all(np.abs(f - golden_edge["d730_f"]) <= 1e-8 * np.abs(golden_edge["d730_f"]))
+
+
+def test_additive_and_flat(eng):
+    ds = synthetic.daily_dates("2015-01-01", "2017-12-31")
+    Y = synthetic.sales_matrix(4, ds, seed=5)
+    for growth, mode in [("linear", "additive"), ("flat", "multiplicative")]:
+        cfg = dfa.ProphetConfig.reference()
+        cfg.growth, cfg.seasonality_mode = growth, mode
+        e2 = dfa.Engine(0, cfg)
+        g = _grid(e2, ds)
+        fit = e2.fit(g, _Y(g, Y))
+        ocfg = dict(po.DEFAULT_CONFIG, growth=growth, seasonality_mode=mode)
+        for s in range(4):
+            setup = po.build_problem(ds, Y[s], ocfg)
+            _, f_o, *_ = so.fit_setup(setup)
+            f = fit.f[s].item()
+            assert f <= f_o + 1e-6 * abs(f_o), (growth, mode, s, f, f_o)
+
+
+# --------------------------------------------------------------- drop-in API
+def test_forecast_store_items_matches_per_group(eng):
+    df = synthetic.store_item_frame(2, 3, "2015-01-01", "2017-12-31")
+    # one series gets NaN history tail (the 2006-row NaN-padded shape of §3.2)
+    m = (df.store == 2) & (df.item == 3) & (df.ds > "2017-10-02")
+    df.loc[m, "y"] = np.nan
+    res = dfa.forecast_store_items(df)
+    assert list(res.columns) == ["ds", "store", "item", "y", "yhat", "yhat_upper", "yhat_lower"]
+    assert res["store"].dtype == np.int32 and res["yhat"].dtype == np.float32
+    assert len(res) == 6 * (1096 + 90)
+    one = df[(df.store == 2) & (df.item == 3)].reset_index(drop=True)
+    r1 = dfa.forecast_store_item(one)
+    sub = res[(res.store == 2) & (res.item == 3)].reset_index(drop=True)
+    assert len(sub) == len(r1) == 1186
+    assert np.array_equal(sub["ds"].values, r1["ds"].values)
+    assert np.allclose(sub["yhat"], r1["yhat"], rtol=1e-6, atol=1e-4)
+    # y copied by position (NaN past the group's rows and where y was NaN)
+    assert np.isnan(sub["y"].values[1096:]).all()
+    assert np.allclose(sub["y"].values[:1000], one["y"].values[:1000])
+    # against the oracle's polished MAP for one fully observed series
+    s2 = df[(df.store == 1) & (df.item == 2)].reset_index(drop=True)
+    ds2 = s2["ds"].values.astype("datetime64[ns]").astype(np.int64)
+    st = po.build_problem(ds2, s2["y"].to_numpy(np.float64))
+    th = so.fit_map(st)[0]
+    pt = po.predict_point(st, po.params_from_theta(th, st.problem.S), B.future_dates(ds2, 90))
+    got = res[(res.store == 1) & (res.item == 2)]["yhat"].to_numpy(np.float64)
+    assert np.max(np.abs(got - pt["yhat"])) / st.hist.y_scale < 1e-5
+
+
+def test_prophet_class_surface(eng):
+    df = synthetic.store_item_frame(1, 1)
+    m = dfa.reference_model()
+    m.fit(df[["ds", "y"]])
+    fut = m.make_future_dataframe(periods=90, freq="d", include_history=True)
+    assert len(fut) == 1916
+    fc = m.predict(fut)
+    assert list(fc.columns) == [
+        "ds", "trend", "yhat_lower", "yhat_upper", "trend_lower", "trend_upper",
+        "multiplicative_terms", "multiplicative_terms_lower", "multiplicative_terms_upper",
+        "weekly", "weekly_lower", "weekly_upper", "yearly", "yearly_lower", "yearly_upper",
+        "additive_terms", "additive_terms_lower", "additive_terms_upper", "yhat"]
+    assert np.allclose(fc["multiplicative_terms"], fc["weekly"] + fc["yearly"], atol=1e-5)
+    assert np.allclose(fc["yhat"], fc["trend"] * (1 + fc["multiplicative_terms"]), rtol=1e-5)
+    assert m.changepoints.shape[0] == 25 and m.params["delta"].shape == (1, 25)
+    with pytest.raises(Exception, match="only be fit once"):
+        m.fit(df[["ds", "y"]])
+    with pytest.raises(ValueError, match="less than 2"):
+        dfa.Prophet().fit(pd.DataFrame({"ds": pd.date_range("2020-01-01", periods=3),
+                                        "y": [1.0, np.nan, np.nan]}))
+
+
+def test_params_store_and_pyfunc(eng, tmp_path):
+    df = synthetic.store_item_frame(2, 2, "2016-01-01", "2017-12-31")
+    store = dfa.ParamsStore(str(tmp_path / "params"))
+    res = dfa.forecast_store_items(df, params_store=store, seed=0)
+    assert len(store) == 4
+    model = dfa.ForecastStoreItemModel(str(tmp_path / "params"), seed=0)
+    model.load_context(None)
+    fut = res[["ds", "store", "item"]]
+    out = model.predict(None, fut)
+    assert list(out.columns) == ["ds", "store", "item", "yhat", "yhat_upper", "yhat_lower"]
+    a = res.sort_values(["store", "item", "ds"]).reset_index(drop=True)
+    b = out.sort_values(["store", "item", "ds"]).reset_index(drop=True)
+    assert np.array_equal(a["ds"].values, b["ds"].values)
+    # same params, same RNG stream key (store, item) and seed -> identical output
+    for k in ("yhat", "yhat_lower", "yhat_upper"):
+        assert np.array_equal(a[k].values, b[k].values), k
+    dfa.register_model(model)
+    one = fut[(fut.store == 1) & (fut.item == 2)].tail(90)
+    r = dfa.predict_udf(one)
+    assert len(r) == 90
+    with pytest.raises(KeyError):
+        model.predict(None, pd.DataFrame({"ds": fut.ds[:3], "store": 9, "item": 9}))
+
+
+def test_cv_metrics_kernel_vs_oracle(eng, golden_ref):
+    ds, Y = golden_ref["ds_ns"], golden_ref["Y"][:2]
+    met = dfa.cv_metrics_batch(eng, ds, Y)
+    names = list(golden_ref["cv_metric_names"])
+    for j, k in enumerate(names):
+        got, want = met[k], golden_ref["cv_metrics"][:, j]
+        assert np.all(np.abs(got - want) <= 1e-4 * np.abs(want)), (k, got, want)
+
+
+def test_cv_metrics_kernel_exact_on_given_rows(eng):
+    """K6 alone: the rolling sweep on fixed inputs equals the oracle's."""
+    import ctypes
+    from distributed_forecasting_amd import _lib as L
+    rng = np.random.default_rng(0)
+    n, folds, H = 5, 3, 90
+    h = np.tile(np.arange(1, H + 1), folds)
+    order = np.argsort(h, kind="stable")
+    hs = h[order]
+    brk = np.flatnonzero(hs[1:] != hs[:-1]) + 1
+    gs = np.concatenate(([0], brk, [len(hs)])).astype(np.int32)
+    y = rng.uniform(1, 50, (n, len(h)))
+    y[4, 7] = 0.0                                         # MAPE skipped for series 4
+    f = (y + rng.normal(0, 3, y.shape)).astype(np.float32)
+    lo, hi = f - 4, f + 4
+    dev = "cuda"
+    yy = torch.from_numpy(y[:, order].copy()).to(dev)
+    ff = torch.from_numpy(f[:, order].copy()).to(dev)
+    ll = torch.from_numpy(lo[:, order].copy()).to(dev)
+    hh = torch.from_numpy(hi[:, order].copy()).to(dev)
+    g = torch.from_numpy(gs).to(dev)
+    met = torch.empty((n, 6), dtype=torch.float64, device=dev)
+    w = int(0.1 * len(h))
+    a = L.PfCvArgs(n, len(h), len(gs) - 1, w, g.data_ptr(), yy.data_ptr(), ff.data_ptr(),
+                   ll.data_ptr(), hh.data_ptr(), met.data_ptr())
+    eng.ctx.check(eng.ctx.lib.pf_cv_metrics(eng.ctx.h, ctypes.byref(a), None), "cv")
+    torch.cuda.synchronize()
+    m = met.cpu().numpy()
+    for s in range(n):
+        pm = po.performance_metrics(y[s], f[s].astype(np.float64), h,
+                                    metrics=("mse", "rmse", "mae", "mape", "smape", "coverage"),
+                                    yhat_lower=lo[s], yhat_upper=hi[s])
+        for j, k in enumerate(["mse", "rmse", "mae", "mape", "smape", "coverage"]):
+            if k not in pm:
+                assert np.isnan(m[s, j])
+            else:
+                assert abs(m[s, j] - np.mean(pm[k])) <= 1e-12 * max(1.0, abs(np.mean(pm[k])))
+
+
+def test_timing_records(eng):
+    ds = synthetic.daily_dates("2016-01-01", "2017-12-31")
+    g = _grid(eng, ds)
+    Y = synthetic.sales_matrix(4, ds)
+    eng.ctx.set_timing(True)
+    fit = eng.fit(g, _Y(g, Y))
+    eng.predict(fit, eng.predict_grid(fit, B.future_dates(ds, 90)))
+    rec = eng.ctx.read_timings()
+    eng.ctx.set_timing(False)
+    names = [r[0] for r in rec]
+    for k in ("k_prepare", "k_fit", "k_polish", "k_predict"):
+        assert k in names
+    assert all(r[1] > 0 for r in rec)

@@ -1,0 +1,130 @@
+"""CPU: host-side logic of the drop-in layer (no kernel launches)."""
+import os
+import re
+import subprocess
+import sys
+
+import numpy as np
+import pandas as pd
+import pytest
+
+import distributed_forecasting_amd as dfa
+from distributed_forecasting_amd import _lib, batch as B, diagnostics, synthetic, training
+from distributed_forecasting_amd.engine import ProphetConfig, NS_PER_DAY
+from oracle import prophet_oracle as po
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_header_symbols_exported():
+    """The C-ABI library loads and exports every function include/prophet_hip.h declares."""
+    hdr = open(os.path.join(ROOT, "include", "prophet_hip.h")).read()
+    decl = set(re.findall(r"^\s*(?:int|void|const char \*)\s*(pf_\w+)\s*\(", hdr, re.M))
+    assert decl == set(_lib.EXPORTED)
+    lib = _lib.load()
+    for name in decl:
+        assert hasattr(lib, name), name
+
+
+def test_num_changepoints_host():
+    for T, want in [(1826, 25), (730, 25), (10, 7), (2, 0), (31, 23), (32, 24), (33, 25)]:
+        assert _lib.num_changepoints(T) == want
+        assert len(po.changepoint_indices(T)) == want
+
+
+def test_missing_library_fails_loudly():
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from distributed_forecasting_amd import _lib\n"
+            "try:\n    _lib.load('/nonexistent/libprophet_hip.so')\n"
+            "except _lib.EngineUnavailable as e:\n    print('UNAVAILABLE')\n") % ROOT
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert "UNAVAILABLE" in out.stdout
+
+
+def test_no_cpu_fallback_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    df = synthetic.store_item_frame(1, 1, "2017-01-01", "2017-03-01")
+    with pytest.raises(RuntimeError, match="no GPU"):
+        dfa.Prophet().fit(df[["ds", "y"]])
+
+
+def test_seasonality_auto_rules():
+    cfg = ProphetConfig()
+    d = NS_PER_DAY
+    assert [s[0] for s in cfg.seasons(0, 1825 * d, d)] == ["yearly", "weekly"]
+    assert [s[0] for s in cfg.seasons(0, 100 * d, d)] == ["weekly"]
+    assert [s[0] for s in cfg.seasons(0, 10 * d, d)] == []
+    assert [s[0] for s in cfg.seasons(0, 5 * d, 3600 * 10**9)] == ["daily"]
+    assert [s[0] for s in cfg.seasons(0, 1825 * d, 7 * d)] == ["yearly"]
+    ref = ProphetConfig.reference()
+    assert ref.seasons(0, 100 * d, d) == [("yearly", 365.25, 10), ("weekly", 7.0, 3)]
+
+
+def test_future_dates_daily():
+    ds = synthetic.daily_dates()
+    fut = B.future_dates(ds, 90)
+    assert len(fut) == 1916
+    assert np.array_equal(fut, po.make_future_dates(ds, 90))
+    assert np.array_equal(fut[1826:] - ds[-1], NS_PER_DAY * np.arange(1, 91))
+
+
+def test_bucket_groups_nan_and_signatures():
+    ds = synthetic.daily_dates("2017-01-01", "2017-01-20")
+    y1 = np.arange(20, dtype=float)
+    y2 = y1 * 2
+    y3 = y1.copy(); y3[5] = np.nan
+    perm = np.random.default_rng(0).permutation(20)
+    bks = B.bucket_groups([ds, ds[perm], ds], [y1, y2[perm], y3])
+    assert len(bks) == 2
+    b0 = [b for b in bks if len(b.members) == 2][0]
+    assert b0.members.tolist() == [0, 1]
+    assert np.array_equal(b0.Y[1], y2)             # sorted by ds
+    b1 = [b for b in bks if len(b.members) == 1][0]
+    assert len(b1.fit_ds) == 19 and len(b1.history_dates) == 20
+    with pytest.raises(ValueError, match="less than 2 non-NaN"):
+        B.bucket_groups([ds[:3]], [np.array([1.0, np.nan, np.nan])])
+
+
+def test_group_frame_keeps_row_order():
+    df = pd.DataFrame({"store": [2, 1, 2, 1, 2], "item": [1, 1, 1, 1, 1],
+                       "ds": pd.date_range("2020-01-01", periods=5), "y": [5., 4., 3., 2., 1.]})
+    keys, rows = training.group_frame(df, ["store", "item"])
+    assert keys.tolist() == [[1, 1], [2, 1]]
+    assert rows[0].tolist() == [1, 3] and rows[1].tolist() == [0, 2, 4]
+
+
+def test_shard_hash_properties():
+    keys = np.stack(np.meshgrid(np.arange(1, 11), np.arange(1, 51), indexing="ij"), -1).reshape(-1, 2)
+    for G in (1, 2, 4, 8):
+        sh = B.shard_of(keys, G)
+        assert sh.min() >= 0 and sh.max() < G
+        counts = np.bincount(sh, minlength=G)
+        assert counts.sum() == 500
+        if G > 1:
+            assert counts.max() < 500 / G * 1.5
+    # stable across calls and independent of the batch it is computed in
+    assert np.array_equal(B.shard_of(keys[:7], 8), B.shard_of(keys, 8)[:7])
+    sid = B.series_id(keys)
+    assert sid.dtype == np.int32 and len(np.unique(sid)) == 500
+
+
+def test_generate_cutoffs_matches_oracle():
+    ds = synthetic.daily_dates()
+    for h, i, p in [(90, 730, 360), (30, 365, 180), (90, 100, 45)]:
+        a = diagnostics.generate_cutoffs(ds, h * NS_PER_DAY, i * NS_PER_DAY, p * NS_PER_DAY)
+        b = po.generate_cutoffs(ds, h * NS_PER_DAY, i * NS_PER_DAY, p * NS_PER_DAY)
+        assert a == b
+    with pytest.raises(ValueError):
+        diagnostics.generate_cutoffs(ds[:50], 90 * NS_PER_DAY, 730 * NS_PER_DAY, 360 * NS_PER_DAY)
+
+
+def test_synthetic_shape_and_determinism():
+    ds = synthetic.daily_dates()
+    assert len(ds) == 1826
+    a = synthetic.sales_matrix(3, ds)
+    b = synthetic.sales_matrix(3, ds)
+    assert np.array_equal(a, b) and a.min() >= 0 and np.all(a == np.round(a))
+    df = synthetic.store_item_frame(2, 3)
+    assert len(df) == 6 * 1826 and df["store"].dtype == np.int32
