@@ -1,0 +1,71 @@
+"""Summarise a tools/profile_round.sh output directory into profiles/.
+
+    python tools/pmc_summary.py gpurun_out/prof_r01 r01
+
+Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --kernel-trace --stats of
+bench.py), profiles/<tag>_pmc.json (per-kernel averages of every counter) and
+profiles/pmc_k_fit.json (the k_fit HBM bytes per launch bench.py reports as
+roofline.traffic).  HBM bytes = 2*FETCH_SIZE + WRITE_SIZE (KiB -> bytes): on
+gfx950 FETCH_SIZE counts half of a wide coalesced read stream
+(MI355X_MICROARCH.md §HBM)."""
+import csv
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+
+def read_counters(path):
+    acc = defaultdict(lambda: defaultdict(list))
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            acc[row["Kernel_Name"]][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    return acc
+
+
+def main(src, tag):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prof = os.path.join(root, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
+                os.path.join(prof, f"{tag}_kernel_stats.csv"))
+    out = defaultdict(dict)
+    with open(os.path.join(src, "trace", "run_kernel_stats.csv")) as f:
+        for row in csv.DictReader(f):
+            out[row["Name"]]["avg_ns"] = float(row["AverageNs"])
+            out[row["Name"]]["calls"] = int(row["Calls"])
+    for sub in ("pmc_fetch", "pmc_write", "pmc_sq"):
+        p = os.path.join(src, sub, "run_counter_collection.csv")
+        if not os.path.exists(p):
+            continue
+        for k, cs in read_counters(p).items():
+            for c, v in cs.items():
+                out[k][c] = sum(v) / len(v)
+    for k, d in out.items():
+        if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+            d["hbm_bytes_per_launch"] = (2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024
+            if "avg_ns" in d:
+                d["hbm_GBps"] = d["hbm_bytes_per_launch"] / d["avg_ns"]
+        if "SQ_WAVE_CYCLES" in d and d["SQ_WAVE_CYCLES"] > 0:
+            w = d["SQ_WAVE_CYCLES"]
+            d["frac_wait_any"] = d.get("SQ_WAIT_ANY", 0) / w
+            d["frac_wait_inst_any"] = d.get("SQ_WAIT_INST_ANY", 0) / w
+            d["frac_active_inst_any"] = d.get("SQ_ACTIVE_INST_ANY", 0) / w
+    with open(os.path.join(prof, f"{tag}_pmc.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+    if "k_fit" in out and "hbm_bytes_per_launch" in out["k_fit"]:
+        with open(os.path.join(prof, "pmc_k_fit.json"), "w") as f:
+            json.dump({"tag": tag, "kernel": "k_fit",
+                       "hbm_bytes_per_launch": out["k_fit"]["hbm_bytes_per_launch"],
+                       "FETCH_SIZE_KiB": out["k_fit"]["FETCH_SIZE"],
+                       "WRITE_SIZE_KiB": out["k_fit"]["WRITE_SIZE"],
+                       "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE half-count)"},
+                      f, indent=1)
+    for k in ("k_fit", "k_polish", "k_predict"):
+        if k in out:
+            print(k, {a: (round(b, 4) if isinstance(b, float) else b) for a, b in out[k].items()})
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
