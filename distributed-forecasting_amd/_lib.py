@@ -21,6 +21,7 @@ PF_ST_CONSTANT = 50
 EXPORTED = ["pf_ctx_create", "pf_ctx_destroy", "pf_last_error", "pf_default_fit_opts",
             "pf_num_changepoints", "pf_build_grid", "pf_prepare", "pf_objective_grad",
             "pf_fit", "pf_predict", "pf_set_timing", "pf_read_timings", "pf_cv_metrics"]
+PF_INTERVAL = {"exact": 0, "sample": 1}
 CV_METRICS = ["mse", "rmse", "mae", "mape", "smape", "coverage"]
 
 
@@ -56,7 +57,7 @@ class PfFitOpts(ctypes.Structure):
 
 
 class PfPredictArgs(ctypes.Structure):
-    _fields_ = [("n_series", i32), ("growth", i32), ("n_samples", i32), ("_pad", i32),
+    _fields_ = [("n_series", i32), ("growth", i32), ("n_samples", i32), ("interval_method", i32),
                 ("fg", PfGrid),
                 ("s_a", vp), ("s_m", vp), ("theta", vp), ("y_scale", vp), ("cap_scaled", vp),
                 ("interval_width", ctypes.c_double), ("seed", ctypes.c_uint64),

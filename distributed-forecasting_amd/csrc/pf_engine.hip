@@ -21,6 +21,7 @@
 #include "pf_common.h"
 #include "prophet_hip.h"
 #include "pf_cv.h"
+#include "pf_ostat.h"
 
 #ifndef M_PI
 #define M_PI 3.14159265358979323846
@@ -1210,7 +1211,6 @@ struct PredKArgs {
   const int32_t *seg;
   const double *s_a, *s_m;
   const double *theta, *y_scale;
-  double t_max, lam_pois;
   int k_lo, k_hi_neg;  // order statistics: lower k_lo,k_lo+1; upper via negation
   float fr_lo, fr_hi;
   uint32_t seed0, seed1;
@@ -1219,6 +1219,7 @@ struct PredKArgs {
   int comp_col0[4], comp_ncol[4];
   float *comp;
   const uint32_t *series_id;  // RNG stream key per series (NULL: batch index)
+  int method;                 // PF_INTERVAL_EXACT / PF_INTERVAL_SAMPLE
 };
 
 // k-th and (k+1)-th smallest of the wave's samples (v[q] = +inf if absent).
@@ -1282,18 +1283,143 @@ __device__ __forceinline__ float np_lerp(float a, float b, float t) {
   return (t >= 0.5f) ? (b - d * (1.0f - t)) : (a + d * t);
 }
 
-// trend offset of MC sample `smp` at time ti (in scaled units):
-// sum over the sample's new changepoints with ti >= t_c of delta_c (ti - t_c)
-__device__ __noinline__ double mc_trend_offset(uint32_t seed0, uint32_t seed1, double lam_pois,
-                                               double t_max, uint32_t series, int smp, double ti,
-                                               double lam) {
+// Per-series forecast state shared by the two forecast kernels (LDS).
+struct PredSeries {
+  double kseg[64], mseg[64], bm[64], ba[64];
+  double sigma, ysc, lam;
+};
+
+// wave 0: theta -> segment rates/offsets, beta*s_m / beta*s_a, sigma, lambda
+__device__ __forceinline__ void pred_setup(const PredKArgs &a, int series, PredSeries &ps) {
+  const int lane = pf_lane();
+  if (pf_wave() != 0) return;
+  const int P = a.P, S = a.S, K = a.K;
+  const double x = (lane < P) ? a.theta[(size_t)series * P + lane] : 0.0;
+  const double k = readlane_f64(x, 0), m = readlane_f64(x, 1);
+  const double dj = __shfl(x, (lane + 2) & 63, 64);
+  const double dval = (lane < S) ? dj : 0.0;
+  const double tcd = (lane < S) ? a.t_change[lane] * dval : 0.0;
+  const double cd = wave_prefix_sum(dval), ctd = wave_prefix_sum(tcd);
+  const double cd_ex = wave_shift_up1(cd), ctd_ex = wave_shift_up1(ctd);
+  if (lane <= S) {
+    ps.kseg[lane] = k + (lane == 0 ? 0.0 : cd_ex);
+    ps.mseg[lane] = m - (lane == 0 ? 0.0 : ctd_ex);
+  }
+  const double bval = __shfl(x, (lane + 3 + S) & 63, 64);
+  const double bv = (lane < K) ? bval : 0.0;
+  ps.bm[lane] = bv * ((lane < K) ? a.s_m[lane] : 0.0);
+  ps.ba[lane] = bv * ((lane < K) ? a.s_a[lane] : 0.0);
+  const double absd = wave_sum(fabs(dval));
+  const double ls = readlane_f64(x, 2 + S);
+  if (lane == 0) {
+    ps.sigma = exp(ls);                   // sigma_obs
+    ps.ysc = a.y_scale[series];
+    ps.lam = absd / (double)S + 1e-8;     // lambda = mean|delta| + 1e-8 (UPSTREAM)
+  }
+}
+
+// UPSTREAM sample_predictive_trend: T = t.max() of the frame being predicted
+// (rows sorted: the last valid row); the trend of a row is random iff
+// growth is linear, T > 1 and t > 1 (new changepoints live on (1, T]).
+__device__ __forceinline__ bool pred_row_random(const PredKArgs &a, double ti, double t_max) {
+  return a.growth == PF_GROWTH_LINEAR && ti > 1.0 && t_max > 1.0;
+}
+
+// ---- K4: point forecast + components + deterministic-row intervals.
+// Grid (ceil(Tf/256), n_series), thread per row.  Under PF_INTERVAL_EXACT
+// the interval endpoints of deterministic rows are exact order-statistic
+// draws (pf_ostat.h); rows left to k_predict_mc are not written here.
+template <int KMAX>
+__global__ __launch_bounds__(256) void k_predict_det(PredKArgs a) {
+  __shared__ PredSeries ps;
+  const int series = blockIdx.y;
+  const uint32_t sid = a.series_id ? a.series_id[series] : (uint32_t)series;
+  pred_setup(a, series, ps);
+  __syncthreads();
+  const int row = blockIdx.x * 256 + threadIdx.x;
+  if (row >= a.Tf) return;
+  const double t_max = a.t[a.Tf - 1];
+  const double ysc = ps.ysc;
+  const double ti = a.t[row];
+  const int sg = a.seg[row];
+  double xbm = 0.0, xba = 0.0;
+  double cb[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int f = 0; f < a.K; ++f) {
+    const double xv = a.XT[(size_t)f * a.Tp + row];
+    const double pm = xv * ps.bm[f], pa = xv * ps.ba[f];
+    xbm += pm;
+    xba += pa;
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+      if (b < a.n_comp && f >= a.comp_col0[b] && f < a.comp_col0[b] + a.comp_ncol[b])
+        cb[b] += pm + pa * ysc;
+  }
+  if (a.comp) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+      if (b < a.n_comp) a.comp[((size_t)b * a.n_series + series) * a.Tp + row] = (float)cb[b];
+  }
+  const double trs = (a.growth == PF_GROWTH_LINEAR) ? (ps.kseg[sg] * ti + ps.mseg[sg]) : ps.mseg[0];
+  const double trend = trs * ysc;
+  const double addt = xba * ysc;
+  const double yhat = trend * (1.0 + xbm) + addt;
+  const size_t o = (size_t)series * a.Tp + row;
+  a.yhat[o] = (float)yhat;
+  if (a.tr) a.tr[o] = (float)trend;
+  if (a.mult) a.mult[o] = (float)xbm;
+  if (a.add) a.add[o] = (float)addt;
+  const bool mc = (a.N > 0) && (a.method == PF_INTERVAL_SAMPLE || pred_row_random(a, ti, t_max));
+  if (mc) return;
+  float ylo = (float)yhat, yhi = (float)yhat;
+  if (a.N > 0) {
+    // exact joint order statistics of the N noise draws (pf_ostat.h)
+    int rk[4] = {a.k_lo + 1, a.k_lo + 2, a.N - a.k_hi_neg - 1, a.N - a.k_hi_neg};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) rk[q] = min(max(rk[q], 1), a.N);
+    pf_rowrng rng{(uint32_t)row, sid, a.seed0, a.seed1, 0u};
+    double z[4];
+    pf_normal_order_stats(rk, a.N, rng, z);
+    const double sd = ps.sigma * ysc;
+    const double fl = (double)a.fr_lo, fh = (double)a.fr_hi;
+    // numpy _lerp on the sorted samples yhat + sd*z
+    const double l0 = yhat + sd * z[0], l1 = yhat + sd * z[1];
+    const double h0 = yhat + sd * z[2], h1 = yhat + sd * z[3];
+    ylo = (float)((fl >= 0.5) ? l1 - (l1 - l0) * (1.0 - fl) : l0 + (l1 - l0) * fl);
+    yhi = (float)((fh >= 0.5) ? h1 - (h1 - h0) * (1.0 - fh) : h0 + (h1 - h0) * fh);
+  }
+  a.ylo[o] = ylo;
+  a.yhi[o] = yhi;
+  if (a.tr) { a.trlo[o] = (float)trend; a.trhi[o] = (float)trend; }
+}
+
+// ---- K5: Monte-Carlo rows.  Grid (G, n_series), 4 waves per block, wave per
+// row (rows r0 + w, r0 + w + 4G, ...).  r0 = first random-trend row (exact)
+// or 0 (sample).  Each block first draws every sample's future changepoints
+// once (Poisson count, uniform times on (1, T], Laplace(λ) rates) into LDS,
+// so a row's 1000 trend offsets cost ~1.2 FMAs each; a sample with more than
+// PF_MC_NCP changepoints (P ≈ 3e-4 at T=1826) re-derives them from its
+// counter-based stream (same draws, evaluated in fp64).
+#define PF_MC_NCP 6
+#define PF_MC_WAVES_PER_SERIES 16
+
+__device__ __forceinline__ void mc_sample_cp(uint32_t seed0, uint32_t seed1, uint32_t series, int smp,
+                                             int c, double t_max, double lam, double &tc, double &dl) {
+  const pf_u4 rc = philox4x32_10(pf_u4{(uint32_t)smp, (uint32_t)(c + 1), (uint32_t)series, 0x7EE2D00Du},
+                                 seed0 ^ 0x5A5A5A5Au, seed1);
+  tc = 1.0 + pf_u01d(rc.x, rc.y) * (t_max - 1.0);
+  const double ul = pf_u01d(rc.z, rc.w);
+  dl = (ul >= 0.5) ? -lam * log(2.0 - ul - ul) : lam * log(ul + ul);
+}
+
+__device__ __forceinline__ int mc_sample_count(uint32_t seed0, uint32_t seed1, uint32_t series, int smp,
+                                               double lam_pois, double e_neg) {
   const pf_u4 r0 = philox4x32_10(pf_u4{(uint32_t)smp, 0u, (uint32_t)series, 0x7EE2D00Du},
                                  seed0 ^ 0x5A5A5A5Au, seed1);
   // Poisson(lam_pois) by inversion
   const double u0 = pf_u01d(r0.x, r0.y);
   int n = 0;
   if (lam_pois > 0.0) {
-    double p = exp(-lam_pois), F = p;
+    double p = e_neg, F = p;
     while (u0 > F && n < 100000) {
       ++n;
       p *= lam_pois / (double)n;
@@ -1301,162 +1427,148 @@ __device__ __noinline__ double mc_trend_offset(uint32_t seed0, uint32_t seed1, d
       if (p == 0.0 && F < u0) break;
     }
   }
+  return n;
+}
+
+__device__ __noinline__ double mc_offset_slow(uint32_t seed0, uint32_t seed1, uint32_t series, int smp,
+                                              int n, double t_max, double lam, double ti) {
   double off = 0.0;
   for (int c = 0; c < n; ++c) {
-    const pf_u4 rc = philox4x32_10(pf_u4{(uint32_t)smp, (uint32_t)(c + 1), (uint32_t)series,
-                                         0x7EE2D00Du},
-                                   seed0 ^ 0x5A5A5A5Au, seed1);
-    const double tc = 1.0 + pf_u01d(rc.x, rc.y) * (t_max - 1.0);
-    const double ul = pf_u01d(rc.z, rc.w);
-    const double lap = (ul >= 0.5) ? -lam * log(2.0 - ul - ul) : lam * log(ul + ul);
-    if (ti >= tc) off += lap * (ti - tc);
+    double tc, dl;
+    mc_sample_cp(seed0, seed1, series, smp, c, t_max, lam, tc, dl);
+    if (ti >= tc) off += dl * (ti - tc);
   }
   return off;
 }
 
-template <int KMAX, int MODE>
-__global__ __launch_bounds__(256) void k_predict(PredKArgs a) {
-  // (a is a by-value copy: t_max / lam_pois are filled in below)
-  __shared__ double s_kseg[64], s_mseg[64], s_bm[64], s_ba[64], s_sc[4];
+template <int KMAX>
+__global__ __launch_bounds__(256) void k_predict_mc(PredKArgs a) {
+  __shared__ PredSeries ps;
+  __shared__ float2 s_cp[PF_MC_NCP][64 * PF_NQ];   // (t_c, delta) per sample
+  __shared__ int s_cnt[64 * PF_NQ];
   __shared__ float s_buf[4][64];
-  __shared__ float s_off[4][64 * PF_NQ];
+  __shared__ int s_r0;
   const int series = blockIdx.y, lane = pf_lane(), wave = pf_wave();
   const uint32_t sid = a.series_id ? a.series_id[series] : (uint32_t)series;
-  const int P = a.P, S = a.S, K = a.K;
-  if (wave == 0) {
-    const double x = (lane < P) ? a.theta[(size_t)series * P + lane] : 0.0;
-    const double k = readlane_f64(x, 0), m = readlane_f64(x, 1);
-    const double dj = __shfl(x, (lane + 2) & 63, 64);
-    const double dval = (lane < S) ? dj : 0.0;
-    const double tcd = (lane < S) ? a.t_change[lane] * dval : 0.0;
-    const double cd = wave_prefix_sum(dval), ctd = wave_prefix_sum(tcd);
-    const double cd_ex = wave_shift_up1(cd), ctd_ex = wave_shift_up1(ctd);
-    if (lane <= S) {
-      s_kseg[lane] = k + (lane == 0 ? 0.0 : cd_ex);
-      s_mseg[lane] = m - (lane == 0 ? 0.0 : ctd_ex);
+  pred_setup(a, series, ps);
+  const double t_max = a.t[a.Tf - 1];
+  if (threadIdx.x == 0) {
+    int r0 = 0;
+    if (a.method != PF_INTERVAL_SAMPLE) {
+      // first random-trend row (rows sorted by t)
+      int lo = 0, hi = a.Tf;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (pred_row_random(a, a.t[mid], t_max)) hi = mid; else lo = mid + 1;
+      }
+      r0 = lo;
     }
-    const double bval = __shfl(x, (lane + 3 + S) & 63, 64);
-    const double bv = (lane < K) ? bval : 0.0;
-    s_bm[lane] = bv * ((lane < K) ? a.s_m[lane] : 0.0);
-    s_ba[lane] = bv * ((lane < K) ? a.s_a[lane] : 0.0);
-    const double absd = wave_sum(fabs(dval));
-    const double ls = readlane_f64(x, 2 + S);
-    if (lane == 0) {
-      s_sc[0] = exp(ls);                            // sigma_obs
-      s_sc[1] = a.y_scale[series];
-      s_sc[2] = absd / (double)S + 1e-8;            // lambda = mean|delta| + 1e-8
+    s_r0 = r0;
+  }
+  __syncthreads();
+  const int r0 = s_r0;
+  if (r0 >= a.Tf) return;
+  const double sigma = ps.sigma, ysc = ps.ysc, lam = ps.lam;
+  const bool any_random = pred_row_random(a, t_max, t_max);
+  const double lam_pois = any_random ? (double)a.S * (t_max - 1.0) : 0.0;
+  if (any_random) {
+    const double e_neg = exp(-lam_pois);
+    for (int smp = threadIdx.x; smp < a.N; smp += 256) {
+      const int n = mc_sample_count(a.seed0, a.seed1, sid, smp, lam_pois, e_neg);
+      s_cnt[smp] = n;
+      for (int c = 0; c < n && c < PF_MC_NCP; ++c) {
+        double tc, dl;
+        mc_sample_cp(a.seed0, a.seed1, sid, smp, c, t_max, lam, tc, dl);
+        s_cp[c][smp] = make_float2((float)tc, (float)dl);
+      }
     }
   }
   __syncthreads();
-  const double sigma = s_sc[0], ysc = s_sc[1], lam = s_sc[2];
-  const bool linear = a.growth == PF_GROWTH_LINEAR;
-  // UPSTREAM sample_predictive_trend: T = t.max() of the frame being predicted
-  // (rows sorted, so the last valid row); Poisson rate S*(T-1) when T > 1.
-  a.t_max = a.t[a.Tf - 1];
-  a.lam_pois = (a.t_max > 1.0) ? (double)S * (a.t_max - 1.0) : 0.0;
-  for (int r = 0; r < 4; ++r) {
-    const int row = blockIdx.x * 16 + wave * 4 + r;
-    if (row >= a.Tf) break;
+  const int stride = gridDim.x * 4;
+  for (int row = r0 + blockIdx.x * 4 + wave; row < a.Tf; row += stride) {
     const double ti = a.t[row];
     const int sg = a.seg[row];
     double xbm = 0.0, xba = 0.0;
-    if (lane < K) {
+    if (lane < a.K) {
       const double xv = a.XT[(size_t)lane * a.Tp + row];
-      xbm = xv * s_bm[lane];
-      xba = xv * s_ba[lane];
-    }
-    if (a.comp) {
-      // per-block components: lanes of block b hold x*beta (mult or add part)
-      const double part = xbm + xba * ysc;
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        if (b < a.n_comp) {
-          const bool inb = lane >= a.comp_col0[b] && lane < a.comp_col0[b] + a.comp_ncol[b];
-          const double cb = wave_sum(inb ? part : 0.0);
-          if (lane == 0) a.comp[((size_t)b * a.n_series + series) * a.Tp + row] = (float)cb;
-        }
-      }
+      xbm = xv * ps.bm[lane];
+      xba = xv * ps.ba[lane];
     }
     xbm = wave_sum(xbm);
     xba = wave_sum(xba);
-    const double trs = linear ? (s_kseg[sg] * ti + s_mseg[sg]) : s_mseg[0];
+    const double trs = (a.growth == PF_GROWTH_LINEAR) ? (ps.kseg[sg] * ti + ps.mseg[sg]) : ps.mseg[0];
     const double trend = trs * ysc;
     const double addt = xba * ysc;
     const double yhat = trend * (1.0 + xbm) + addt;
-    float ylo = (float)yhat, yhi = (float)yhat, tlo = (float)trend, thi = (float)trend;
-    if (a.N > 0) {
-      float z[PF_NQ];
+    float ylo, yhi, tlo = (float)trend, thi = (float)trend;
+    float z[PF_NQ];
 #pragma unroll
-      for (int c = 0; c < PF_NQ / 4; ++c) {
-        const pf_u4 rr = philox4x32_10(pf_u4{(uint32_t)c, (uint32_t)lane, (uint32_t)row, sid},
-                                       a.seed0, a.seed1);
-        pf_box_muller(pf_u01f(rr.x), pf_u01f(rr.y), z[4 * c + 0], z[4 * c + 1]);
-        pf_box_muller(pf_u01f(rr.z), pf_u01f(rr.w), z[4 * c + 2], z[4 * c + 3]);
+    for (int c = 0; c < PF_NQ / 4; ++c) {
+      const pf_u4 rr = philox4x32_10(pf_u4{(uint32_t)c, (uint32_t)lane, (uint32_t)row, sid},
+                                     a.seed0, a.seed1);
+      pf_box_muller(pf_u01f(rr.x), pf_u01f(rr.y), z[4 * c + 0], z[4 * c + 1]);
+      pf_box_muller(pf_u01f(rr.z), pf_u01f(rr.w), z[4 * c + 2], z[4 * c + 3]);
+    }
+    const float sd = (float)(sigma * ysc);
+    const float u1 = (float)(1.0 + xbm);
+    const float addf = (float)addt;
+    float v[PF_NQ], tv[PF_NQ];
+    const bool random = pred_row_random(a, ti, t_max);
+    if (!random) {
+      const float base = (float)yhat;
+#pragma unroll
+      for (int q = 0; q < PF_NQ; ++q) {
+        const int smp = lane + 64 * q;
+        v[q] = (smp < a.N) ? fmaf(sd, z[q], base) : INFINITY;
       }
-      const float sd = (float)(sigma * ysc);
-      const float u1 = (float)(1.0 + xbm);
-      const float addf = (float)addt;
-      float v[PF_NQ], tv[PF_NQ];
-      const bool future = linear && (ti > 1.0) && (a.t_max > 1.0);
-      if (!future) {
-        const float base = (float)yhat;
+    } else {
+      const float tf = (float)ti, ysf = (float)ysc;
 #pragma unroll
-        for (int q = 0; q < PF_NQ; ++q) {
-          const int smp = lane + 64 * q;
-          v[q] = (smp < a.N) ? fmaf(sd, z[q], base) : INFINITY;
-        }
-      } else {
-        // per-sample trend offsets (rolled loop; keeps the code small)
-        float *offs = s_off[wave];
-#pragma unroll 1
-        for (int q = 0; q < PF_NQ; ++q) {
-          const int smp = lane + 64 * q;
-          offs[q * 64 + lane] = (smp < a.N) ? (float)(ysc * mc_trend_offset(a.seed0, a.seed1, a.lam_pois, a.t_max, sid, smp, ti, lam)) : 0.0f;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int q = 0; q < PF_NQ; ++q) {
-          const int smp = lane + 64 * q;
-          if (smp < a.N) {
-            const float trs_s = (float)trend + offs[q * 64 + lane];
-            tv[q] = trs_s;
-            v[q] = fmaf(sd, z[q], fmaf(trs_s, u1, addf));
+      for (int q = 0; q < PF_NQ; ++q) {
+        const int smp = lane + 64 * q;
+        if (smp < a.N) {
+          const int n = s_cnt[smp];
+          float off = 0.0f;
+          if (n <= PF_MC_NCP) {
+            for (int c = 0; c < n; ++c) {
+              const float2 cp = s_cp[c][smp];
+              off = (tf >= cp.x) ? fmaf(cp.y, tf - cp.x, off) : off;
+            }
           } else {
-            tv[q] = INFINITY;
-            v[q] = INFINITY;
+            off = (float)mc_offset_slow(a.seed0, a.seed1, sid, smp, n, t_max, lam, ti);
           }
+          const float trs_s = (float)trend + ysf * off;
+          tv[q] = trs_s;
+          v[q] = fmaf(sd, z[q], fmaf(trs_s, u1, addf));
+        } else {
+          tv[q] = INFINITY;
+          v[q] = INFINITY;
         }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
       }
-      float* buf = s_buf[wave];
-      float a0, a1;
-      wave_select_pair(v, a.k_lo, buf, a0, a1);
-      ylo = np_lerp(a0, a1, a.fr_lo);
-      float nv[PF_NQ];
+    }
+    float *buf = s_buf[wave];
+    float a0, a1;
+    wave_select_pair(v, a.k_lo, buf, a0, a1);
+    ylo = np_lerp(a0, a1, a.fr_lo);
+    float nv[PF_NQ];
 #pragma unroll
-      for (int q = 0; q < PF_NQ; ++q) nv[q] = (v[q] == INFINITY) ? INFINITY : -v[q];
+    for (int q = 0; q < PF_NQ; ++q) nv[q] = (v[q] == INFINITY) ? INFINITY : -v[q];
+    wave_select_pair(nv, a.k_hi_neg, buf, a0, a1);
+    // a0 = -s[k_hi+1], a1 = -s[k_hi]
+    yhi = np_lerp(-a1, -a0, a.fr_hi);
+    if (random) {
+      wave_select_pair(tv, a.k_lo, buf, a0, a1);
+      tlo = np_lerp(a0, a1, a.fr_lo);
+#pragma unroll
+      for (int q = 0; q < PF_NQ; ++q) nv[q] = (tv[q] == INFINITY) ? INFINITY : -tv[q];
       wave_select_pair(nv, a.k_hi_neg, buf, a0, a1);
-      // a0 = -s[k_hi+1], a1 = -s[k_hi]
-      yhi = np_lerp(-a1, -a0, a.fr_hi);
-      if (future) {
-        wave_select_pair(tv, a.k_lo, buf, a0, a1);
-        tlo = np_lerp(a0, a1, a.fr_lo);
-#pragma unroll
-        for (int q = 0; q < PF_NQ; ++q) nv[q] = (tv[q] == INFINITY) ? INFINITY : -tv[q];
-        wave_select_pair(nv, a.k_hi_neg, buf, a0, a1);
-        thi = np_lerp(-a1, -a0, a.fr_hi);
-      }
+      thi = np_lerp(-a1, -a0, a.fr_hi);
     }
     if (lane == 0) {
       const size_t o = (size_t)series * a.Tp + row;
-      a.yhat[o] = (float)yhat;
       a.ylo[o] = ylo;
       a.yhi[o] = yhi;
-      if (a.tr) { a.tr[o] = (float)trend; a.trlo[o] = tlo; a.trhi[o] = thi; }
-      if (a.mult) a.mult[o] = (float)xbm;
-      if (a.add) a.add[o] = (float)addt;
+      if (a.tr) { a.trlo[o] = tlo; a.trhi[o] = thi; }
     }
   }
 }
@@ -1822,10 +1934,24 @@ int pf_predict(pf_ctx *ctx, const pf_predict_args *p, void *stream) {
     a.fr_hi = (float)(ihi - khi);
     if (a.N == 1) { a.k_lo = 0; a.fr_lo = 0.f; a.k_hi_neg = 0; a.fr_hi = 0.f; }
   }
-  const dim3 grid((a.Tf + 15) / 16, a.n_series);
-  PF_TIMED_LAUNCH(ctx, "k_predict", grid.x * grid.y, (hipStream_t)stream,
-                  (k_predict<64, MODE_MIXED>), grid, dim3(256), 0, (hipStream_t)stream, a);
+  a.method = p->interval_method;
+  if (a.method != PF_INTERVAL_EXACT && a.method != PF_INTERVAL_SAMPLE)
+    return set_err(ctx, "pf_predict: interval_method must be PF_INTERVAL_EXACT or PF_INTERVAL_SAMPLE");
+  const dim3 grid((a.Tf + 255) / 256, a.n_series);
+  PF_TIMED_LAUNCH(ctx, "k_predict_det", grid.x * grid.y, (hipStream_t)stream,
+                  (k_predict_det<64>), grid, dim3(256), 0, (hipStream_t)stream, a);
   PF_HIP(ctx, hipGetLastError());
+  if (a.N > 0) {
+    // sample mode: ~8 rows per wave; exact mode: the random rows (the
+    // horizon) spread over PF_MC_WAVES_PER_SERIES waves per series
+    int gx = (a.method == PF_INTERVAL_SAMPLE) ? (a.Tf + 31) / 32 : PF_MC_WAVES_PER_SERIES / 4;
+    if (gx > (a.Tf + 3) / 4) gx = (a.Tf + 3) / 4;
+    if (gx < 1) gx = 1;
+    const dim3 gmc(gx, a.n_series);
+    PF_TIMED_LAUNCH(ctx, "k_predict_mc", gmc.x * gmc.y, (hipStream_t)stream,
+                    (k_predict_mc<64>), gmc, dim3(256), 0, (hipStream_t)stream, a);
+    PF_HIP(ctx, hipGetLastError());
+  }
   return 0;
 }
 

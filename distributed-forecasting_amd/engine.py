@@ -46,6 +46,10 @@ class ProphetConfig:
     changepoint_prior_scale: float = 0.05
     interval_width: float = 0.80
     uncertainty_samples: int = 1000
+    # engine option (no Prophet counterpart): how deterministic-trend rows get
+    # their interval endpoints — "exact" order statistics of the N draws (same
+    # distribution, O(1) per row) or "sample" (materialise all N draws)
+    interval_method: str = "exact"
 
     @classmethod
     def reference(cls) -> "ProphetConfig":
@@ -334,7 +338,8 @@ class Engine:
 
     def predict(self, fit: FitResult, fgrid: DeviceGrid, n_samples: int | None = None,
                 seed: int = 0, components: bool = True,
-                series_id: torch.Tensor | None = None) -> dict:
+                series_id: torch.Tensor | None = None,
+                interval_method: str | None = None) -> dict:
         """Point forecast + MC intervals for every fitted series on ``fgrid``.
         Returns float32 device tensors [n, fgrid.T_pad] (valid columns :T).
         ``series_id`` (int32/uint32 [n] on the device) keys each series' RNG
@@ -353,6 +358,10 @@ class Engine:
         a.n_series = n
         a.growth = L.PF_GROWTH[self.config.growth]
         a.n_samples = int(ns)
+        im = self.config.interval_method if interval_method is None else interval_method
+        if im not in L.PF_INTERVAL:
+            raise ValueError(f"interval_method must be one of {sorted(L.PF_INTERVAL)}")
+        a.interval_method = L.PF_INTERVAL[im]
         a.fg = fgrid.as_pf()
         a.s_a, a.s_m = s_a.data_ptr(), s_m.data_ptr()
         a.theta = fit.theta.data_ptr()

@@ -157,8 +157,17 @@ int pf_fit(pf_ctx *ctx, const pf_problem *pb, const pf_fit_opts *opts,
  * t_change).  Outputs fp32 [n*fg.T_pad] (stride T_pad).  n_samples <= 1024;
  * n_samples == 0 skips the intervals (lower/upper = point).  trend_* and
  * the component outputs may be NULL.                                     */
+/* Interval estimator (pf_predict_args.interval_method).
+ *  EXACT  (0, default): rows whose trend is deterministic (the history, flat
+ *         growth) draw the needed order statistics of the N noise samples
+ *         exactly (uniform spacings + inverse normal CDF): the same
+ *         distribution as N materialised samples, O(1) work per row.  Rows
+ *         with future trend uncertainty are always sampled N times.
+ *  SAMPLE (1): every row materialises N samples (UPSTREAM's literal loop). */
+enum { PF_INTERVAL_EXACT = 0, PF_INTERVAL_SAMPLE = 1 };
+
 typedef struct {
-  int32_t n_series, growth, n_samples, _pad;
+  int32_t n_series, growth, n_samples, interval_method;
   pf_grid fg;
   const double *s_a, *s_m;
   const double *theta;        /* [n*P] */

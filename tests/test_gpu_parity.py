@@ -137,12 +137,13 @@ def test_fit_without_polish_is_stan_faithful(eng, golden_ref):
 
 
 # --------------------------------------------------------- K5 intervals
-def test_intervals_within_mc_error(eng, golden_ref):
+@pytest.mark.parametrize("method", ["exact", "sample"])
+def test_intervals_within_mc_error(eng, golden_ref, method):
     ds, Y, fut = golden_ref["ds_ns"], golden_ref["Y"], golden_ref["fut_ns"]
     g = _grid(eng, ds)
     fit = eng.fit(g, _Y(g, Y))
     fg = eng.predict_grid(fit, fut)
-    out = eng.predict(fit, fg, seed=11)
+    out = eng.predict(fit, fg, seed=11, interval_method=method)
     ysc = np.abs(Y).max(1)
     for s in range(8):
         sd = np.exp(golden_ref["theta_map"][s, 27]) * ysc[s]
@@ -162,15 +163,49 @@ def test_intervals_within_mc_error(eng, golden_ref):
         assert np.allclose(tlo[:1826], thi[:1826], rtol=0, atol=1e-4 * ysc[s])
 
 
-def test_interval_coverage_history(eng, golden_ref):
+@pytest.mark.parametrize("method", ["exact", "sample"])
+def test_interval_coverage_history(eng, golden_ref, method):
     ds, Y = golden_ref["ds_ns"], golden_ref["Y"]
     g = _grid(eng, ds)
     fit = eng.fit(g, _Y(g, Y))
-    out = eng.predict(fit, eng.predict_grid(fit, ds), seed=3)
+    out = eng.predict(fit, eng.predict_grid(fit, ds), seed=3, interval_method=method)
     lo = out["yhat_lower"][:, :len(ds)].cpu().numpy()
     hi = out["yhat_upper"][:, :len(ds)].cpu().numpy()
     cov = np.mean((Y >= lo) & (Y <= hi))
     assert 0.90 < cov < 0.98
+
+
+def test_exact_intervals_same_law_as_sampled(eng, golden_ref):
+    """History rows: the exact order-statistic draw (PF_INTERVAL_EXACT) and the
+    literal 1000-sample estimate (PF_INTERVAL_SAMPLE, UPSTREAM's loop) are two
+    draws of the same random variable.  Compare the normalised endpoints
+    e = (bound - yhat)/sd over all 8 x 1826 history rows: two-sample KS, mean
+    and spread (theory for N=1000, 2.5 %: mean -1.9505, sd 0.0838)."""
+    from scipy import stats
+    ds, Y, fut = golden_ref["ds_ns"], golden_ref["Y"], golden_ref["fut_ns"]
+    g = _grid(eng, ds)
+    fit = eng.fit(g, _Y(g, Y))
+    fg = eng.predict_grid(fit, fut)
+    th = fit.theta.cpu().numpy()
+    sd = np.exp(th[:, 2 + g.S]) * fit.y_scale.cpu().numpy()
+    res = {}
+    for m in ("exact", "sample"):
+        o = eng.predict(fit, fg, seed=5, interval_method=m, components=False)
+        yh = o["yhat"][:, :1826].double().cpu().numpy()
+        lo = (o["yhat_lower"][:, :1826].double().cpu().numpy() - yh) / sd[:, None]
+        hi = (o["yhat_upper"][:, :1826].double().cpu().numpy() - yh) / sd[:, None]
+        res[m] = (lo.ravel(), hi.ravel(), o)
+    for i in (0, 1):
+        a, b = res["exact"][i], res["sample"][i]
+        assert stats.ks_2samp(a, b).pvalue > 1e-4
+        assert abs(a.mean() - b.mean()) < 0.01
+        assert abs(abs(a.mean()) - 1.9505) < 0.006
+        assert 0.075 < a.std() < 0.093 and 0.075 < b.std() < 0.093
+    # independent of the history rows' method, the future rows are sampled
+    # identically (same RNG streams) and the point forecast is identical
+    oe, os_ = res["exact"][2], res["sample"][2]
+    assert torch.equal(oe["yhat"][:, :fg.T], os_["yhat"][:, :fg.T])
+    assert torch.equal(oe["yhat_lower"][:, 1826:fg.T], os_["yhat_lower"][:, 1826:fg.T])
 
 
 def test_predict_seed_and_series_id(eng, golden_ref):
@@ -389,6 +424,6 @@ def test_timing_records(eng):
     rec = eng.ctx.read_timings()
     eng.ctx.set_timing(False)
     names = [r[0] for r in rec]
-    for k in ("k_prepare", "k_fit", "k_polish", "k_predict"):
+    for k in ("k_prepare", "k_fit", "k_polish", "k_predict_det", "k_predict_mc"):
         assert k in names
     assert all(r[1] > 0 for r in rec)

@@ -147,3 +147,28 @@ def test_rolling_mean_by_h_small():
     hs, v = po.rolling_mean_by_h(np.array([1., 3., 5., 7., 9.]), np.array([1, 1, 2, 3, 3]), 2)
     assert hs.tolist() == [1, 2, 3]
     assert np.allclose(v, [2.0, 3.5, 8.0])   # h=2: (5 + 4 - 1 * 4/2) / 2
+
+
+def test_order_statistic_spacings_match_sampling():
+    """Math behind PF_INTERVAL_EXACT (csrc/pf_ostat.h): the joint law of the
+    normal order statistics at ranks (25, 26, 975, 976) of N = 1000 draws,
+    built from Gamma spacings + the inverse normal CDF, equals brute-force
+    sorting, checked through np.percentile(·, 2.5 / 97.5) ('linear')."""
+    from scipy import stats
+    from scipy.special import ndtri
+    N, M = 1000, 6000
+    rng = np.random.default_rng(20261016)
+    Z = rng.standard_normal((M, N))
+    bl, bh = np.percentile(Z, 2.5, axis=1), np.percentile(Z, 97.5, axis=1)
+    ilo, ihi = N * 0.025 + 0.975 - 1, N * 0.975 + 0.025 - 1
+    klo, khi = int(ilo), int(ihi)
+    r = [klo + 1, klo + 2, khi + 1, khi + 2]
+    shapes = [r[0], r[1] - r[0], r[2] - r[1], r[3] - r[2], N + 1 - r[3]]
+    G = np.stack([rng.gamma(s, size=M) for s in shapes], 1)
+    U = np.cumsum(G, 1)[:, :4] / G.sum(1)[:, None]
+    z = ndtri(U)
+    el = z[:, 0] + (z[:, 1] - z[:, 0]) * (ilo - klo)
+    eh = z[:, 2] + (z[:, 3] - z[:, 2]) * (ihi - khi)
+    assert stats.ks_2samp(bl, el).pvalue > 1e-3
+    assert stats.ks_2samp(bh, eh).pvalue > 1e-3
+    assert stats.ks_2samp(bh - bl, eh - el).pvalue > 1e-3

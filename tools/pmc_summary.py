@@ -62,7 +62,7 @@ def main(src, tag):
                        "WRITE_SIZE_KiB": out["k_fit"]["WRITE_SIZE"],
                        "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE half-count)"},
                       f, indent=1)
-    for k in ("k_fit", "k_polish", "k_predict"):
+    for k in ("k_fit", "k_polish", "k_predict_det", "k_predict_mc"):
         if k in out:
             print(k, {a: (round(b, 4) if isinstance(b, float) else b) for a, b in out[k].items()})
 
