@@ -81,6 +81,29 @@ __device__ __forceinline__ double shfl_xor_f64(double x) {
                                           __float_as_uint(lo)));
 }
 
+// Pairwise cross-half/cross-row adds: one permlane swap per dword exchanges
+// the halves of two registers, so no keep/send selects are needed.
+//   pair_add32(a, b): lanes 0..31 -> a_l + a_{l+32}, lanes 32..63 -> b_{l-32} + b_l
+//   pair_add16(a, b): rows 0,2 -> a_l + a_{l+16}, rows 1,3 -> b_{l-16} + b_l
+__device__ __forceinline__ double pair_add32(double a, double b) {
+  const unsigned long long ua = (unsigned long long)__double_as_longlong(a);
+  const unsigned long long ub = (unsigned long long)__double_as_longlong(b);
+  const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)ua, (unsigned)ub, false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(ua >> 32), (unsigned)(ub >> 32), false, false);
+  const double x = __longlong_as_double((long long)(((unsigned long long)hi[0] << 32) | lo[0]));
+  const double y = __longlong_as_double((long long)(((unsigned long long)hi[1] << 32) | lo[1]));
+  return x + y;
+}
+__device__ __forceinline__ double pair_add16(double a, double b) {
+  const unsigned long long ua = (unsigned long long)__double_as_longlong(a);
+  const unsigned long long ub = (unsigned long long)__double_as_longlong(b);
+  const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)ua, (unsigned)ub, false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(ua >> 32), (unsigned)(ub >> 32), false, false);
+  const double x = __longlong_as_double((long long)(((unsigned long long)hi[0] << 32) | lo[0]));
+  const double y = __longlong_as_double((long long)(((unsigned long long)hi[1] << 32) | lo[1]));
+  return x + y;
+}
+
 // full-wave sum, result uniform in every lane
 __device__ __forceinline__ double wave_sum(double v) {
   v += dpp_f64<PF_DPP_QXOR1>(v);
@@ -134,25 +157,28 @@ __device__ __forceinline__ void wave_sum_multi(const double (&v)[N], double (&ou
   const int lane = pf_lane();
   double w16[16], w8[8], w4[4], w2[2], w1;
   // level xor 32: value pair (2k, 2k+1) -> lanes <32 keep 2k, >=32 keep 2k+1
-  const bool h5 = lane & 32, h4 = lane & 16, h3 = lane & 8, h2 = lane & 4, h1 = lane & 2;
+  // (pairs whose value indices are all >= N are skipped at compile time)
+  const bool h3 = lane & 8, h2 = lane & 4, h1 = lane & 2;
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    const double a = (2 * k < N) ? v[2 * k] : 0.0, b = (2 * k + 1 < N) ? v[2 * k + 1] : 0.0;
-    const double keep = h5 ? b : a, send = h5 ? a : b;
-    w16[k] = keep + shfl_xor_f64<32>(send);
+    if (2 * k >= N) { w16[k] = 0.0; continue; }
+    const double a = v[2 * k], b = (2 * k + 1 < N) ? v[2 * k + 1] : 0.0;
+    w16[k] = pair_add32(a, b);
   }
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    const double keep = h4 ? w16[2 * k + 1] : w16[2 * k], send = h4 ? w16[2 * k] : w16[2 * k + 1];
-    w8[k] = keep + shfl_xor_f64<16>(send);
+    if (4 * k >= N) { w8[k] = 0.0; continue; }
+    w8[k] = pair_add16(w16[2 * k], w16[2 * k + 1]);
   }
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
+    if (8 * k >= N) { w4[k] = 0.0; continue; }
     const double keep = h3 ? w8[2 * k + 1] : w8[2 * k], send = h3 ? w8[2 * k] : w8[2 * k + 1];
     w4[k] = keep + shfl_xor_f64<8>(send);
   }
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
+    if (16 * k >= N) { w2[k] = 0.0; continue; }
     const double keep = h2 ? w4[2 * k + 1] : w4[2 * k], send = h2 ? w4[2 * k] : w4[2 * k + 1];
     w2[k] = keep + shfl_xor_f64<4>(send);
   }
@@ -167,6 +193,67 @@ __device__ __forceinline__ void wave_sum_multi(const double (&v)[N], double (&ou
     const int l = ((idx & 1) << 5) | (((idx >> 1) & 1) << 4) | (((idx >> 2) & 1) << 3) |
                   (((idx >> 3) & 1) << 2) | (((idx >> 4) & 1) << 1);
     out[idx] = readlane_f64(w1, l);
+  }
+}
+
+// Transposed wave reduction of N <= 64 per-lane values by recursive halving
+// (about N shuffle+add pairs instead of 6 per value).  Returns, in every
+// lane, the wave total of value index transpose_index<N>(lane); for N <= 32
+// the two lanes of each (2k, 2k+1) pair hold the same total.
+template <int N>
+__device__ __forceinline__ int transpose_index(int lane) {
+  if constexpr (N <= 32)
+    return ((lane >> 5) & 1) | (((lane >> 4) & 1) << 1) | (((lane >> 3) & 1) << 2) |
+           (((lane >> 2) & 1) << 3) | (((lane >> 1) & 1) << 4);
+  else
+    return ((lane >> 5) & 1) | (((lane >> 4) & 1) << 1) | (((lane >> 3) & 1) << 2) |
+           (((lane >> 2) & 1) << 3) | (((lane >> 1) & 1) << 4) | ((lane & 1) << 5);
+}
+template <int M, int D, int N>
+__device__ __forceinline__ void transpose_level(const double (&w)[M], double (&o)[M / 2]) {
+  const bool h = pf_lane() & D;
+  constexpr int SPAN = (M == 64) ? 1 : 32 / M;  // value indices per input entry
+#pragma unroll
+  for (int k = 0; k < M / 2; ++k) {
+    // value indices carried by w[2k], w[2k+1] are all >= N: compile-time zero
+    if (2 * k * SPAN >= N) { o[k] = 0.0; continue; }
+    const double a = w[2 * k], b = w[2 * k + 1];
+    if constexpr (D == 32) {
+      o[k] = pair_add32(a, b);
+    } else if constexpr (D == 16) {
+      o[k] = pair_add16(a, b);
+    } else {
+      const double keep = h ? b : a, send = h ? a : b;
+      o[k] = keep + shfl_xor_f64<D>(send);
+    }
+  }
+}
+template <int N>
+__device__ __forceinline__ double wave_transpose_sum(const double (&v)[N]) {
+  static_assert(N >= 1 && N <= 64, "wave_transpose_sum: 1 <= N <= 64");
+  if constexpr (N <= 32) {
+    double w32[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) w32[i] = (i < N) ? v[i] : 0.0;
+    double w16[16], w8[8], w4[4], w2[2], w1[1];
+    transpose_level<32, 32, N>(w32, w16);
+    transpose_level<16, 16, N>(w16, w8);
+    transpose_level<8, 8, N>(w8, w4);
+    transpose_level<4, 4, N>(w4, w2);
+    transpose_level<2, 2, N>(w2, w1);
+    return w1[0] + shfl_xor_f64<1>(w1[0]);
+  } else {
+    double w64[64];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) w64[i] = (i < N) ? v[i] : 0.0;
+    double w32[32], w16[16], w8[8], w4[4], w2[2], w1[1];
+    transpose_level<64, 32, N>(w64, w32);
+    transpose_level<32, 16, N>(w32, w16);
+    transpose_level<16, 8, N>(w16, w8);
+    transpose_level<8, 4, N>(w8, w4);
+    transpose_level<4, 2, N>(w4, w2);
+    transpose_level<2, 1, N>(w2, w1);
+    return w1[0];
   }
 }
 

@@ -274,6 +274,12 @@ struct FitKArgs {
   int T, Tp, K, S, growth, P, NB;
   const double *t, *XT, *t_change;
   const int32_t *seg;
+  // lane-blocked copy of the grid (k_permute_grid): thread L of the
+  // workgroup owns natural rows [L*R, L*R+R); position r*NL + L holds row
+  // L*R + r, so step r of the row pass is a coalesced load across lanes.
+  int R, TQ;                 // rows per thread, TQ = NL*R
+  const double *tP, *XTP;    // [TQ], [K][TQ]
+  const int32_t *sgP;        // [TQ] seg | (#changepoints first active at this row) << 16
   const double *sigmas, *s_a, *s_m;
   double tau;
   const double *y_scaled;
@@ -315,6 +321,23 @@ struct RowIn {
   int seg, sprev;
   double f[6];  // first-harmonic (sin, cos) of up to three Fourier blocks
 };
+
+// lane-blocked layout: position q of the permuted grid
+template <int O0, int O1, int O2>
+__device__ __forceinline__ void load_rowp(const FitKArgs &a, int q, RowIn &r) {
+  const int TQ = a.TQ;
+  r.t = a.tP[q];
+  const int pk = a.sgP[q];
+  r.seg = pk & 0xFFFF;
+  r.sprev = r.seg - (pk >> 16);
+  const double *X = a.XTP;
+  if constexpr (O0 > 0) { r.f[0] = X[q]; r.f[1] = X[(size_t)TQ + q]; }
+  if constexpr (O1 > 0) { r.f[2] = X[(size_t)(2 * O0) * TQ + q]; r.f[3] = X[(size_t)(2 * O0 + 1) * TQ + q]; }
+  if constexpr (O2 > 0) {
+    r.f[4] = X[(size_t)(2 * (O0 + O1)) * TQ + q];
+    r.f[5] = X[(size_t)(2 * (O0 + O1) + 1) * TQ + q];
+  }
+}
 
 template <int O0, int O1, int O2>
 __device__ __forceinline__ void load_row(const double *__restrict__ t, const int32_t *__restrict__ seg,
@@ -372,72 +395,82 @@ __device__ __forceinline__ void row_features(const double *__restrict__ XT, int 
 
 static constexpr size_t kLbBytes = 9 * 1024;
 struct LbLds;
-// LDS layout of the fit kernel.  Fixed part + a union region U that holds
-// {beta-gradient partials, L-BFGS state} during the Stan phase and
-// {Hessian tile reduction, H, Cholesky workspace} during the polish.
+// LDS layout of the fit kernels.  Fixed part + a union region U that holds
+// the L-BFGS state during the Stan phase (k_fit) and {Hessian tile
+// reduction, H, Cholesky workspace} during the polish (k_polish).
 template <int NW, int KMAX, int MODE = 2>
 struct FitSmem {
-  static constexpr int NSET = 2;  // (mult, add) partial-set slots (index by set)
-  double *y;        // [Tp]
+  static constexpr int NSET = (MODE == 2) ? 2 : 1;  // (mult, add) gradient sets
+  static constexpr int NL = NW * 64;                 // row-pass threads
+  double *y;        // [ny] lane-blocked y_scaled (position r*NL + L)
   double *th;       // [64]
   double *kseg;     // [64]
   double *mseg;     // [64]
   double *bm, *ba;  // [KMAX]
-  double *bsum0, *bsum1;  // [NB]
-  double *cps0, *cps1;    // [64]
+  double *sfx0, *sfx1;    // [NL] inclusive within-wave suffix of per-thread sums of G, G*t
+  double *wt0, *wt1;      // [NW] per-wave totals of G, G*t
+  double *cpre0, *cpre1;  // [64] per changepoint: owner thread's sum before its first row
   double *rrw;      // [NW]
   double *gout;     // [64]
   double *fout;     // [4]
-  double *gb;       // [2][KMAX] reduced
+  double *sig;      // [2] sigma, 1/sigma^2 of the published point
+  double *gpart;    // [NW][NSET*KMAX] per-wave beta-gradient totals
   double *pd, *pz;  // [64] polish direction / scratch
-  int *cpb;         // [64]
+  int *cpl;         // [64] per changepoint: owner thread
   int *qmap;        // [64]
+  int *flag;        // [4] loop control
+  double *ctc, *csg, *csm, *csa;  // [64] t_change[j], sigmas[f], s_m[f], s_a[f] (0 past the end)
   double *U;        // union region
-  double *gbt;      // U view: [NW][NSET][KMAX][32]
-  struct LbLds *lb; // U view, after gbt
+  struct LbLds *lb; // U view (Stan phase)
   int LD;           // stride of H / M in U (polish)
-  static __host__ __device__ size_t fixed_doubles(int Tp, int NB) {
-    return (size_t)Tp + 64 * 3 + 2 * KMAX + 2 * (size_t)NB + 128 + NW + 64 + 4 + 2 * KMAX + 128 + 64;
+  static __host__ __device__ size_t fixed_doubles(int ny) {
+    return (size_t)ny + 64 * 3 + 2 * KMAX + 2 * NL + 2 * NW + 128 + NW + 64 + 4 + 2 +
+           (size_t)NW * NSET * KMAX + 128 + 32 + 32 + 4 + 4 * 64;
   }
-  // MULT / ADD use one partial set, MIXED two
-  static __host__ __device__ size_t gbt_doubles() { return (size_t)NW * (MODE == 2 ? 2 : 1) * KMAX * 32; }
-  static __host__ __device__ size_t union_bytes(int P) {
-    const size_t eval = gbt_doubles() * sizeof(double) + kLbBytes;
+  static __host__ __device__ size_t union_bytes(int P, bool polish) {
+    if (!polish) return kLbBytes;
     const size_t tiles = (size_t)10 * 4 * 64 * sizeof(double);
     const int LD = P | 1;
     const size_t hm = 2 * (size_t)P * LD * sizeof(double);
-    size_t u = eval > tiles ? eval : tiles;
+    size_t u = kLbBytes > tiles ? kLbBytes : tiles;
     return u > hm ? u : hm;
   }
-  static __host__ __device__ size_t bytes(int Tp, int NB, int P) {
-    return fixed_doubles(Tp, NB) * sizeof(double) + union_bytes(P) + 64;
+  static __host__ __device__ size_t bytes(int ny, int P, bool polish) {
+    return fixed_doubles(ny) * sizeof(double) + union_bytes(P, polish) + 64;
   }
-  __device__ void carve(char *base, int Tp, int NB, int P) {
+  __device__ void carve(char *base, int ny, int P) {
     double *p = reinterpret_cast<double *>(base);
-    y = p; p += Tp;
+    y = p; p += ny;
     th = p; p += 64;
     kseg = p; p += 64;
     mseg = p; p += 64;
     bm = p; p += KMAX;
     ba = p; p += KMAX;
-    bsum0 = p; p += NB;
-    bsum1 = p; p += NB;
-    cps0 = p; p += 64;
-    cps1 = p; p += 64;
+    sfx0 = p; p += NL;
+    sfx1 = p; p += NL;
+    wt0 = p; p += NW;
+    wt1 = p; p += NW;
+    cpre0 = p; p += 64;
+    cpre1 = p; p += 64;
     rrw = p; p += NW;
     gout = p; p += 64;
     fout = p; p += 4;
-    gb = p; p += 2 * KMAX;
+    sig = p; p += 2;
+    gpart = p; p += (size_t)NW * NSET * KMAX;
     pd = p; p += 64;
     pz = p; p += 64;
-    cpb = reinterpret_cast<int *>(p); p += 32;
+    cpl = reinterpret_cast<int *>(p); p += 32;
     qmap = reinterpret_cast<int *>(p); p += 32;
+    flag = reinterpret_cast<int *>(p); p += 4;
+    ctc = p; p += 64;
+    csg = p; p += 64;
+    csm = p; p += 64;
+    csa = p; p += 64;
     // 16-byte align U via offsets from the LDS base (keeps the address space)
     size_t off = (size_t)(reinterpret_cast<char *>(p) - base);
     off = (off + 15) & ~(size_t)15;
     U = reinterpret_cast<double *>(base + off);
-    gbt = U;
-    lb = reinterpret_cast<struct LbLds *>(reinterpret_cast<char *>(U) + gbt_doubles() * sizeof(double));
+    lb = reinterpret_cast<struct LbLds *>(U);
     LD = P | 1;
   }
 };
@@ -452,7 +485,7 @@ __device__ __forceinline__ void publish_theta(const FitKArgs &a, FitSmem<NW, KMA
   // delta_j sits in lane 2+j
   const double dj = __shfl(x, (lane + 2) & 63, 64);
   const double dval = (lane < S) ? dj : 0.0;
-  const double tcd = (lane < S) ? a.t_change[lane] * dval : 0.0;
+  const double tcd = sm.ctc[lane] * dval;
   const double cd = wave_prefix_sum(dval);   // inclusive: sum_{j<=lane}
   const double ctd = wave_prefix_sum(tcd);
   // kseg[s] = k + sum_{j<s} delta_j ; mseg[s] = m - sum_{j<s} tc_j delta_j
@@ -465,26 +498,59 @@ __device__ __forceinline__ void publish_theta(const FitKArgs &a, FitSmem<NW, KMA
   const double bval = __shfl(x, (lane + 3 + S) & 63, 64);
   if (lane < KMAX) {
     const double bv = (lane < K) ? bval : 0.0;
-    sm.bm[lane] = bv * ((lane < K) ? a.s_m[lane] : 0.0);
-    sm.ba[lane] = bv * ((lane < K) ? a.s_a[lane] : 0.0);
+    sm.bm[lane] = bv * sm.csm[lane];
+    sm.ba[lane] = bv * sm.csa[lane];
+  }
+  if (lane == 2 + S) {
+    const double sigma = exp(x);
+    sm.sig[0] = sigma;
+    sm.sig[1] = 1.0 / (sigma * sigma);
   }
 }
 
-// One collective evaluation of f(theta) = -log posterior and its gradient.
-// Every thread of the workgroup must call it.  `x` is this lane's parameter
-// (lane p < P); returns f in every thread and g (lane p) in `g`; returns true
-// if f or g is not finite (Stan ModelAdaptor error → line-search retreat).
+// per-lane problem constants -> LDS once per kernel (every thread calls; the
+// caller's next barrier publishes them)
+template <int NW, int KMAX, int MODE>
+__device__ __forceinline__ void load_consts(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm) {
+  const int i = threadIdx.x;
+  if (i < 64) {
+    sm.ctc[i] = (i < a.S) ? a.t_change[i] : 0.0;
+    sm.csg[i] = (i < a.K) ? a.sigmas[i] : 1.0;
+    sm.csm[i] = (i < a.K) ? a.s_m[i] : 0.0;
+    sm.csa[i] = (i < a.K) ? a.s_a[i] : 0.0;
+  }
+}
+
+// Wave totals of N per-lane values stored to dst[0..N) (chunks of <= 64).
+template <int N, int C0>
+__device__ __forceinline__ void transpose_store(const double (&v)[N], double *dst) {
+  constexpr int CH = (N - C0 > 64) ? 64 : N - C0;
+  double w[CH];
+#pragma unroll
+  for (int i = 0; i < CH; ++i) w[i] = v[C0 + i];
+  const double t = wave_transpose_sum<CH>(w);
+  const int lane = pf_lane();
+  const int idx = transpose_index<CH>(lane);
+  if (idx < CH && (CH > 32 || (lane & 1) == 0)) dst[C0 + idx] = t;
+  if constexpr (C0 + CH < N) transpose_store<N, C0 + CH>(v, dst);
+}
+
+// Row pass of one evaluation (every wave; theta already published).
+// Thread L owns the contiguous natural rows [L*R, L*R + R) (lane-blocked
+// grid, coalesced loads) and accumulates, in registers: the residual sum of
+// squares, its beta-gradient partials, and the running sums of
+// G = r(1 + Xb_m) and G*t.  The changepoint gradient needs suffix sums of
+// G / G*t from each changepoint's first row; the owner thread records its
+// running sums just before that row (cpre), and one scan over thread totals
+// per evaluation (sfx, wt) completes them in eval_assemble.  Leaves its
+// partial results in LDS; the caller synchronises.
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
-__device__ bool eval_collective(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, double x, double &f,
-                                double &g) {
+__device__ __forceinline__ void eval_rows(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm) {
   const int lane = pf_lane(), wave = pf_wave();
-  const int P = a.P, S = a.S, K = a.K, T = a.T, Tp = a.Tp;
-  // ---- phase 0: wave 0 publishes theta and the segment rates/offsets
-  PF_STAMP(0);
-  publish_theta<NW, KMAX, MODE>(a, sm, x);
-  __syncthreads();
+  constexpr int NL = NW * 64;
+  const int L = threadIdx.x;
+  const int K = a.K, T = a.T, R = a.R, TQ = a.TQ;
   PF_STAMP(1);
-  // ---- phase 1: row pass (batch of 64 consecutive rows per wave iteration)
   double gbm[KMAX], gba[KMAX];
 #pragma unroll
   for (int f2 = 0; f2 < KMAX; ++f2) {
@@ -500,19 +566,19 @@ __device__ bool eval_collective(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, 
   }
   const double th_m = sm.th[1];
   const bool linear = (a.growth == PF_GROWTH_LINEAR);
-  double rr = 0.0;
+  double rr = 0.0, acc0 = 0.0, acc1 = 0.0;
   RowIn cur;
-  if (wave < a.NB) load_row<O0, O1, O2>(a.t, a.seg, a.XT, Tp, wave * 64 + lane, cur);
-  for (int b = wave; b < a.NB; b += NW) {
-    const int i = b * 64 + lane;
+  if (R > 0) load_rowp<O0, O1, O2>(a, L, cur);
+  for (int r = 0; r < R; ++r) {
+    const int q = r * NL + L;       // lane-blocked position
+    const int i = L * R + r;        // natural row
     RowIn nxt;
-    if (b + NW < a.NB) load_row<O0, O1, O2>(a.t, a.seg, a.XT, Tp, (b + NW) * 64 + lane, nxt);
+    if (r + 1 < R) load_rowp<O0, O1, O2>(a, q + NL, nxt);
     const bool valid = i < T;
     const double ti = cur.t;
     const int sg = cur.seg;
-    const int sprev = cur.sprev;
     double xf[KMAX];
-    row_features_from<KMAX, O0, O1, O2>(cur, a.XT, Tp, K, i, xf);
+    row_features_from<KMAX, O0, O1, O2>(cur, a.XTP, TQ, K, q, xf);
     double xm[4] = {0.0, 0.0, 0.0, 0.0}, xa[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int f2 = 0; f2 < KMAX; ++f2) {
@@ -524,158 +590,162 @@ __device__ bool eval_collective(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, 
     const double tr = linear ? fma(sm.kseg[sg], ti, sm.mseg[sg]) : th_m;
     const double u = 1.0 + xbm;
     const double mu = fma(tr, u, xba);
-    const double r = valid ? (sm.y[i] - mu) : 0.0;
-    rr = fma(r, r, rr);
-    const double G = r * u;
-    const double cm = r * tr;
+    const double res = valid ? (sm.y[q] - mu) : 0.0;
+    rr = fma(res, res, rr);
+    const double G = res * u;
+    const double cm = res * tr;
 #pragma unroll
     for (int f2 = 0; f2 < KMAX; ++f2) {
       if constexpr (MODE != MODE_ADD) gbm[f2] = fma(xf[f2], cm, gbm[f2]);
-      if constexpr (MODE != MODE_MULT) gba[f2] = fma(xf[f2], r, gba[f2]);
+      if constexpr (MODE != MODE_MULT) gba[f2] = fma(xf[f2], res, gba[f2]);
     }
-    // suffix sums of G and G*t inside the batch; batch totals + cp rows to LDS
-    double tot0, tot1;
-    const double s0 = wave_suffix_sum(G, tot0);
-    const double s1 = wave_suffix_sum(G * ti, tot1);
-    if (lane == 0) {
-      sm.bsum0[b] = tot0;
-      sm.bsum1[b] = tot1;
-    }
-    if (valid && sg > sprev) {
-      for (int j = sprev; j < sg; ++j) {
-        sm.cps0[j] = s0;
-        sm.cps1[j] = s1;
-        sm.cpb[j] = b;
+    // changepoints j in [sprev, sg) are first active at this row
+    if (valid && sg > cur.sprev) {
+      for (int j = cur.sprev; j < sg; ++j) {
+        sm.cpre0[j] = acc0;
+        sm.cpre1[j] = acc1;
+        sm.cpl[j] = L;
       }
     }
+    acc0 += G;
+    acc1 = fma(G, ti, acc1);
     cur = nxt;
   }
   PF_STAMP(2);
-  // ---- phase 2: transpose-reduce the beta gradient partials through LDS
-  // (one permlane32 step first: 32 partials per feature per wave)
+  // thread totals -> inclusive suffix within the wave + wave totals
+  double w0, w1;
+  const double s0 = wave_suffix_sum(acc0, w0);
+  const double s1 = wave_suffix_sum(acc1, w1);
+  sm.sfx0[L] = s0;
+  sm.sfx1[L] = s1;
   rr = wave_sum(rr);
-  if (lane == 0) sm.rrw[wave] = rr;
-  {
-    constexpr int NS = (MODE == MODE_MIXED) ? 2 : 1;
-    double *gw = sm.gbt + (size_t)wave * NS * KMAX * 32;
-#pragma unroll
-    for (int f2 = 0; f2 < KMAX; ++f2) {
-      if constexpr (MODE != MODE_ADD) {
-        const double v = gbm[f2] + shfl_xor_f64<32>(gbm[f2]);
-        if (lane < 32) gw[f2 * 32 + lane] = v;
-      }
-      if constexpr (MODE != MODE_MULT) {
-        const double v = gba[f2] + shfl_xor_f64<32>(gba[f2]);
-        if (lane < 32) gw[((MODE == MODE_MIXED ? KMAX : 0) + f2) * 32 + lane] = v;
-      }
-    }
+  if (lane == 0) {
+    sm.wt0[wave] = w0;
+    sm.wt1[wave] = w1;
+    sm.rrw[wave] = rr;
   }
-  __syncthreads();
-  {
-    // feature f handled by 8 threads, each summing NW*4 partials
-    constexpr int NSET = (MODE == MODE_MIXED) ? 2 : 1;
-    const int tid = threadIdx.x;
-    for (int job = tid; job < NSET * KMAX * 8; job += NW * 64) {
-      const int fs = job >> 3, part = job & 7;
-      const int set = (MODE == MODE_ADD) ? 1 : (fs / KMAX);
-      const int f2 = fs % KMAX;
-      double acc = 0.0;
-      for (int w2 = 0; w2 < NW; ++w2) {
-        constexpr int NS2 = (MODE == MODE_MIXED) ? 2 : 1;
-        const int sset = (MODE == MODE_MIXED) ? set : 0;
-        const double *src = sm.gbt + ((size_t)w2 * NS2 * KMAX + sset * KMAX + f2) * 32 + part * 4;
+  // beta-gradient partials: transposed in-register reduction, one total per lane
+  constexpr int NS = (MODE == MODE_MIXED) ? 2 : 1;
+  double vv[NS * KMAX];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) acc += src[q];
-      }
-      acc += shfl_xor_f64<1>(acc);
-      acc += shfl_xor_f64<2>(acc);
-      acc += shfl_xor_f64<4>(acc);
-      if (part == 0) sm.gb[set * KMAX + f2] = acc;
-    }
+  for (int f2 = 0; f2 < KMAX; ++f2) {
+    if constexpr (MODE == MODE_MULT) vv[f2] = gbm[f2];
+    else if constexpr (MODE == MODE_ADD) vv[f2] = gba[f2];
+    else { vv[f2] = gbm[f2]; vv[KMAX + f2] = gba[f2]; }
   }
-  __syncthreads();
+  transpose_store<NS * KMAX, 0>(vv, sm.gpart + (size_t)wave * NS * KMAX);
   PF_STAMP(3);
-  // ---- phase 3: wave 0 assembles f and g
+}
+
+// Sums of two per-lane values over the wave in one 6-level pass (a is
+// reduced in lanes 0..31, b in lanes 32..63); uniform results via readlane.
+__device__ __forceinline__ void wave_sum2(double a, double b, double &ta, double &tb) {
+  double w = pair_add32(a, b);
+  w += shfl_xor_f64<16>(w);
+  w += shfl_xor_f64<8>(w);
+  w += shfl_xor_f64<4>(w);
+  w += shfl_xor_f64<2>(w);
+  w += shfl_xor_f64<1>(w);
+  ta = readlane_f64(w, 0);
+  tb = readlane_f64(w, 32);
+}
+
+// Wave 0 after the row pass (and a barrier): objective f and gradient g at
+// this lane's parameter x (lane p < P), and gp = g . pdir (the line search's
+// directional derivative; pass pdir = 0 if unused).  Returns true if f or g
+// is not finite (Stan ModelAdaptor error -> line-search retreat).
+template <int NW, int KMAX, int MODE>
+__device__ __forceinline__ bool eval_assemble(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, double x,
+                                              double pdir, double &f, double &g, double &gp) {
+  const int lane = pf_lane();
+  const int P = a.P, S = a.S, T = a.T;
+  const bool linear = (a.growth == PF_GROWTH_LINEAR);
+  double rrt = 0.0, tot0 = 0.0, tot1 = 0.0;
+#pragma unroll
+  for (int w2 = 0; w2 < NW; ++w2) {
+    rrt += sm.rrw[w2];
+    tot0 += sm.wt0[w2];
+    tot1 += sm.wt1[w2];
+  }
+  const double sigma = sm.sig[0], inv_s2 = sm.sig[1];
+  const double ls = x;  // meaningful in lane 2+S only
+  double gv = 0.0, fterm = 0.0;
+  const int p = lane;
+  if (p == 0) {
+    const double k = x;
+    gv = (linear ? -inv_s2 * tot1 : 0.0) + k / 25.0;
+    fterm = k * k / 50.0;
+  } else if (p == 1) {
+    const double m = x;
+    gv = -inv_s2 * tot0 + m / 25.0;
+    fterm = m * m / 50.0;
+  } else if (p < 2 + S) {
+    // suffix sums from changepoint j's first row: owner thread's inclusive
+    // within-wave suffix + later waves - the owner's sum before that row
+    const int j = p - 2;
+    const int Lj = sm.cpl[j];
+    const int wj = Lj >> 6;
+    double l0 = 0.0, l1 = 0.0;
+#pragma unroll
+    for (int w2 = 0; w2 < NW; ++w2)
+      if (w2 > wj) { l0 += sm.wt0[w2]; l1 += sm.wt1[w2]; }
+    const double su0 = (sm.sfx0[Lj] + l0) - sm.cpre0[j];
+    const double su1 = (sm.sfx1[Lj] + l1) - sm.cpre1[j];
+    const double gdel = su1 - sm.ctc[j] * su0;
+    const double d = x;
+    const double sg = (d > 0.0) - (d < 0.0);
+    gv = (linear ? -inv_s2 * gdel : 0.0) + sg / a.tau;
+    fterm = fabs(d) / a.tau;
+  } else if (p == 2 + S) {
+    gv = (double)T - inv_s2 * rrt + 4.0 * sigma * sigma;
+    fterm = 2.0 * sigma * sigma + (double)T * ls;
+  } else if (p < P) {
+    constexpr int NS = (MODE == MODE_MIXED) ? 2 : 1;
+    const int f2 = p - 3 - S;
+    const double bv = x;
+    const double sgm = sm.csg[f2];
+    double gm = 0.0, ga = 0.0;
+#pragma unroll
+    for (int w2 = 0; w2 < NW; ++w2) {
+      const double *gq = sm.gpart + (size_t)w2 * NS * KMAX;
+      if constexpr (MODE == MODE_MULT) gm += gq[f2];
+      else if constexpr (MODE == MODE_ADD) ga += gq[f2];
+      else { gm += gq[f2]; ga += gq[KMAX + f2]; }
+    }
+    double gl = 0.0;
+    if (MODE != MODE_ADD) gl += sm.csm[f2] * gm;
+    if (MODE != MODE_MULT) gl += sm.csa[f2] * ga;
+    gv = -inv_s2 * gl + bv / (sgm * sgm);
+    fterm = bv * bv / (2.0 * sgm * sgm);
+  }
+  g = (p < P) ? gv : 0.0;
+  double fs;
+  wave_sum2(fterm, g * pdir, fs, gp);
+  f = fs + 0.5 * rrt * inv_s2;
+  bool bad = !isfinite(f);
+  if (p < P && !isfinite(gv)) bad = true;
+  return __ballot(bad) != 0ull;
+}
+
+// One collective evaluation of f(theta) = -log posterior and its gradient
+// (K2 / polish).  Every thread of the workgroup must call it.  `x` is this
+// lane's parameter (lane p < P); returns f in every thread and g (lane p).
+template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
+__device__ bool eval_collective(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, double x, double &f,
+                                double &g) {
+  const int lane = pf_lane(), wave = pf_wave();
+  PF_STAMP(0);
+  publish_theta<NW, KMAX, MODE>(a, sm, x);
+  __syncthreads();
+  eval_rows<NW, KMAX, O0, O1, O2, MODE>(a, sm);
+  __syncthreads();
   if (wave == 0) {
-    double rrt = 0.0;
-    for (int w2 = 0; w2 < NW; ++w2) rrt += sm.rrw[w2];
-    // BS[b] = sum_{b' >= b} bsum[b'] (lane = batch when NB <= 64)
-    double tot0, tot1, BS0 = 0.0, BS1 = 0.0;
-    if (a.NB <= 64) {
-      const double v0 = (lane < a.NB) ? sm.bsum0[lane] : 0.0;
-      const double v1 = (lane < a.NB) ? sm.bsum1[lane] : 0.0;
-      BS0 = wave_suffix_sum(v0, tot0);
-      BS1 = wave_suffix_sum(v1, tot1);
-    } else {
-      double l0 = 0.0, l1 = 0.0;
-      for (int bb = lane; bb < a.NB; bb += 64) { l0 += sm.bsum0[bb]; l1 += sm.bsum1[bb]; }
-      tot0 = wave_sum(l0);
-      tot1 = wave_sum(l1);
-    }
-    const double ls = readlane_f64(x, 2 + S);
-    const double sigma = exp(ls);
-    const double inv_s2 = 1.0 / (sigma * sigma);
-    // SU_j (at lane 2+j): cps_j + sum of the batches after cp j's batch
-    double gdel = 0.0;
-    {
-      const int j = lane - 2;  // delta_j lives at lane 2+j
-      const bool has = (j >= 0 && j < S);
-      const int bj1 = has ? sm.cpb[j] + 1 : 63;
-      double later0, later1;
-      if (a.NB <= 64) {
-        // gather BS[bj+1] (0 past the end): one bpermute per evaluation
-        const double g0 = __shfl(BS0, bj1 & 63, 64), g1 = __shfl(BS1, bj1 & 63, 64);
-        later0 = (bj1 < a.NB) ? g0 : 0.0;
-        later1 = (bj1 < a.NB) ? g1 : 0.0;
-      } else {
-        later0 = later1 = 0.0;
-        if (has)
-          for (int bb = bj1; bb < a.NB; ++bb) { later0 += sm.bsum0[bb]; later1 += sm.bsum1[bb]; }
-      }
-      if (has) {
-        const double su0 = sm.cps0[j] + later0;
-        const double su1 = sm.cps1[j] + later1;
-        gdel = su1 - a.t_change[j] * su0;
-      }
-    }
-    double gv = 0.0, fterm = 0.0;
-    const int p = lane;
-    if (p == 0) {
-      const double k = x;
-      gv = (linear ? -inv_s2 * tot1 : 0.0) + k / 25.0;
-      fterm = k * k / 50.0;
-    } else if (p == 1) {
-      const double m = x;
-      gv = -inv_s2 * tot0 + m / 25.0;
-      fterm = m * m / 50.0;
-    }
-    const double gd_here = gdel;
-    if (p >= 2 && p < 2 + S) {
-      const double d = x;
-      const double sg = (d > 0.0) - (d < 0.0);
-      gv = (linear ? -inv_s2 * gd_here : 0.0) + sg / a.tau;
-      fterm = fabs(d) / a.tau;
-    } else if (p == 2 + S) {
-      gv = (double)T - inv_s2 * rrt + 4.0 * sigma * sigma;
-      fterm = 2.0 * sigma * sigma + (double)T * ls;
-    } else if (p > 2 + S && p < P) {
-      const int f2 = p - 3 - S;
-      const double bv = x;
-      const double sgm = a.sigmas[f2];
-      double gl = 0.0;
-      if (MODE != MODE_ADD) gl += a.s_m[f2] * sm.gb[f2];
-      if (MODE != MODE_MULT) gl += a.s_a[f2] * sm.gb[KMAX + f2];
-      gv = -inv_s2 * gl + bv / (sgm * sgm);
-      fterm = bv * bv / (2.0 * sgm * sgm);
-    }
-    const double fsum = wave_sum(fterm) + 0.5 * rrt * inv_s2;
-    bool bad = !isfinite(fsum);
-    if (p < P && !isfinite(gv)) bad = true;
-    const unsigned long long anybad = __ballot(bad);
-    if (p < 64) sm.gout[p] = (p < P) ? gv : 0.0;
+    double fw, gw, gpw;
+    const bool badw = eval_assemble<NW, KMAX, MODE>(a, sm, x, 0.0, fw, gw, gpw);
+    sm.gout[lane] = gw;
     if (lane == 0) {
-      sm.fout[0] = fsum;
-      sm.fout[1] = anybad ? 1.0 : 0.0;
+      sm.fout[0] = fw;
+      sm.fout[1] = badw ? 1.0 : 0.0;
     }
   }
   __syncthreads();
@@ -689,8 +759,15 @@ __device__ bool eval_collective(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, 
 
 template <int NW, int KMAX, int MODE>
 __device__ __forceinline__ void load_y(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, int s) {
+  // lane-blocked copy: position r*NL + L holds natural row L*R + r
   const double *ys = a.y_scaled + (size_t)s * a.Tp;
-  for (int i = threadIdx.x; i < a.Tp; i += NW * 64) sm.y[i] = ys[i];
+  constexpr int NL = NW * 64;
+  const int L = threadIdx.x;
+  for (int r = 0; r < a.R; ++r) {
+    const int i = L * a.R + r;
+    sm.y[r * NL + L] = (i < a.T) ? ys[i] : 0.0;
+  }
+  load_consts<NW, KMAX, MODE>(a, sm);
 }
 
 // ---------------------------------------------------------------- K2 kernel
@@ -698,7 +775,7 @@ template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
 __global__ __launch_bounds__(NW * 64) void k_objgrad(FitKArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   FitSmem<NW, KMAX, MODE> sm;
-  sm.carve(smem_raw, a.Tp, a.NB, a.P);
+  sm.carve(smem_raw, a.TQ, a.P);
   const int s = blockIdx.x, lane = pf_lane();
   load_y<NW, KMAX, MODE>(a, sm, s);
   const double x = (lane < a.P) ? a.theta[(size_t)s * a.P + lane] : 0.0;
@@ -775,8 +852,12 @@ __device__ __forceinline__ int pf_wrap(int a, int H) {
 struct LbLds {
   double xk[64], gk[64], pk[64];
   double hs[PF_HIST][64], hy[PF_HIST][64];   // circular, logical j at (head + j) % H
-  double SY[PF_HIST][PF_HIST];                // s_i . y_j (logical order; upper part used)
-  double YY[PF_HIST][PF_HIST];                // y_i . y_j
+  // compact-form blocks in logical order (oldest = 0), zero beyond the
+  // history length so the 5x5 solves run branch-free
+  double Rm[PF_HIST][PF_HIST];                // Rm[i][j] = s_i . y_j (i <= j used)
+  double YYm[PF_HIST][PF_HIST];               // y_i . y_j
+  double rinv[PF_HIST];                       // 1 / (s_i . y_i)
+  double av[PF_HIST], bv[PF_HIST];            // s_i . g_k, y_i . g_k at the current iterate
   LbScalars z;
   int state;
   int need;
@@ -787,7 +868,7 @@ struct LbLds {
 // evaluation requested last time.
 __device__ __forceinline__ bool lbfgs_step(const pf_fit_opts &o, LbLds &L, int &state, LbScalars &z,
                                            double &xk, double &gk, double &pk, double &xq, double gq,
-                                           bool bad) {
+                                           double gpq, bool bad) {
   const int lane = pf_lane();
   const int H = o.history < PF_HIST ? o.history : PF_HIST;
   while (true) {
@@ -846,7 +927,7 @@ __device__ __forceinline__ bool lbfgs_step(const pf_fit_opts &o, LbLds &L, int &
         }
         z.lsRestarts = 0;
         const double f1 = z.fq;
-        const double newDFp = ddot(gq, pk);
+        const double newDFp = gpq;  // g(x + alpha p) . p, fused into the evaluation
         if ((f1 > z.fk + z.alpha1 * z.c1dfp) || (f1 >= z.prevF && z.nits > 0)) {
           z.alo = z.alpha0; z.aloF = z.prevF; z.aloDFp = z.prevDFp;
           z.ahi = z.alpha1; z.ahiF = f1; z.ahiDFp = newDFp;
@@ -895,7 +976,7 @@ __device__ __forceinline__ bool lbfgs_step(const pf_fit_opts &o, LbLds &L, int &
           return true;  // stay in LB_ZOOM_RES
         }
         const double f1 = z.fq;
-        const double newDFp = ddot(gq, pk);
+        const double newDFp = gpq;
         if (f1 > (z.fk + z.alpha * z.c1dfp) || f1 >= z.aloF) {
           z.ahi = z.alpha; z.ahiF = f1; z.ahiDFp = newDFp;
           state = LB_ZOOM_ITER;
@@ -922,17 +1003,21 @@ __device__ __forceinline__ bool lbfgs_step(const pf_fit_opts &o, LbLds &L, int &
         gk = gq;
         z.alphak_1 = z.alpha;
         z.dfp_prev = z.dfp;
-        // LBFGSUpdate history after this update: clear on reset, drop the
-        // oldest pair when full; kept pairs are old logical j + drop
+        // LBFGSUpdate history after this update: cleared on reset, oldest pair
+        // dropped when full; kept pairs are old logical j + drop
         const int m_old = z.resetB ? 0 : z.hcount;
         const int drop = (m_old == H) ? 1 : 0;
         const int nw = m_old - drop;  // logical index of the new pair
-        // one fused reduction for every inner product this step needs
-        double v[22], r[22];
+        // one fused reduction: gg, ss, sy, yy, s.g, y.g of the new pair and
+        // s_j.y, y_j.y of the kept pairs (their s_j.g, y_j.g follow by
+        // a_j += s_j.y, b_j += y_j.y since g_new = g_old + y)
+        double v[14], r[14];
         v[0] = gq * gq;
         v[1] = sk * sk;
         v[2] = sk * yk;
         v[3] = yk * yk;
+        v[4] = sk * gq;
+        v[5] = yk * gq;
 #pragma unroll
         for (int j = 0; j < PF_HIST - 1; ++j) {
           double sj = 0.0, yj = 0.0;
@@ -941,14 +1026,10 @@ __device__ __forceinline__ bool lbfgs_step(const pf_fit_opts &o, LbLds &L, int &
             sj = L.hs[slot][lane];
             yj = L.hy[slot][lane];
           }
-          v[4 + 2 * j] = sj * yk;
-          v[5 + 2 * j] = yj * yk;
-          v[12 + 2 * j] = sj * gq;
-          v[13 + 2 * j] = yj * gq;
+          v[6 + 2 * j] = sj * yk;
+          v[7 + 2 * j] = yj * yk;
         }
-        v[20] = sk * gq;
-        v[21] = yk * gq;
-        wave_sum_multi<22>(v, r);
+        wave_sum_multi<14>(v, r);
         PF_STAMP(11);
         const double gg = r[0];
         if (fabs(z.fk1 - z.fk) < o.tol_obj) {
@@ -963,95 +1044,97 @@ __device__ __forceinline__ bool lbfgs_step(const pf_fit_opts &o, LbLds &L, int &
                    o.tol_rel_obj * 2.220446049250313e-16) {
           z.ret = PF_ST_RELF;
         } else {
-          // ---- LBFGSUpdate::update, compact form (Byrd-Nocedal-Schnabel):
-          //      H g = gamma g + S p' - gamma Y u,  u = R^-1 a,
-          //      p' = R^-T ((D + gamma Y'Y) u - gamma b),  a = S'g, b = Y'g,
-          //      R = upper(S'Y), D = diag(S'Y), gamma = s'y / y'y (newest pair).
-          //      Identical to Stan's two-loop recursion in exact arithmetic.
+          // ---- LBFGSUpdate::update + search_direction in compact
+          //      (Byrd-Nocedal-Schnabel) form, equal to Stan's two-loop
+          //      recursion in exact arithmetic:
+          //        H g = gamma g + S p' - gamma Y u,  u = R^-1 a,
+          //        p' = R^-T ((D + gamma Y'Y) u - gamma b),  a = S'g, b = Y'g,
+          //      R = upper(S'Y), D = diag(S'Y), gamma = s'y / y'y (newest).
           z.gammak = r[2] / r[3];
           const double gam = z.gammak;
-          // small matrices in registers for this step (static indices)
-          double SYr[PF_HIST][PF_HIST], YYr[PF_HIST][PF_HIST];
-#pragma unroll
-          for (int i = 0; i < PF_HIST; ++i)
-#pragma unroll
-            for (int j = 0; j < PF_HIST; ++j) {
-              const int ii = (i + drop < PF_HIST) ? i + drop : PF_HIST - 1;
-              const int jj = (j + drop < PF_HIST) ? j + drop : PF_HIST - 1;
-              SYr[i][j] = L.SY[ii][jj];
-              YYr[i][j] = L.YY[ii][jj];
+          {
+            // lanes (i, j) < 25 rebuild the logical blocks: reset -> zero,
+            // drop -> shift up-left by one (zero fill), then the new column
+            const int i0 = lane / PF_HIST, j0 = lane - i0 * PF_HIST;
+            double rv = 0.0, yv = 0.0, iv = 0.0, aj = 0.0, bj = 0.0;
+            if (lane < PF_HIST * PF_HIST && !z.resetB) {
+              const int si = i0 + drop, sj = j0 + drop;
+              if (si < PF_HIST && sj < PF_HIST) { rv = L.Rm[si][sj]; yv = L.YYm[si][sj]; }
             }
+            if (lane < PF_HIST && !z.resetB && lane + drop < PF_HIST) {
+              iv = L.rinv[lane + drop];
+              aj = L.av[lane + drop];
+              bj = L.bv[lane + drop];
+            }
+            // new column nw / diagonal, and a_j, b_j moved to g_new
+            double syi = 0.0, yyi = 0.0, yyj = 0.0;
+#pragma unroll
+            for (int j = 0; j < PF_HIST - 1; ++j) {
+              if (i0 == j) { syi = r[6 + 2 * j]; yyi = r[7 + 2 * j]; }
+              if (j0 == j) yyj = r[7 + 2 * j];
+            }
+            if (lane < PF_HIST * PF_HIST) {
+              if (j0 == nw && i0 < nw) { rv = syi; yv = yyi; }
+              if (i0 == nw && j0 < nw) { yv = yyj; }
+              if (i0 == nw && j0 == nw) { rv = r[2]; yv = r[3]; }
+            }
+            if (lane < PF_HIST) {
+              double sy_l = 0.0, yy_l = 0.0;
+#pragma unroll
+              for (int j = 0; j < PF_HIST - 1; ++j)
+                if (lane == j) { sy_l = r[6 + 2 * j]; yy_l = r[7 + 2 * j]; }
+              if (lane < nw) { aj += sy_l; bj += yy_l; }
+              if (lane == nw) { aj = r[4]; bj = r[5]; iv = 1.0 / r[2]; }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            if (lane < PF_HIST * PF_HIST) { L.Rm[i0][j0] = rv; L.YYm[i0][j0] = yv; }
+            if (lane < PF_HIST) { L.rinv[lane] = iv; L.av[lane] = aj; L.bv[lane] = bj; }
+          }
           if (drop) z.head = pf_wrap(z.head + 1, H);
           const int slot_new = pf_wrap(z.head + nw, H);
           L.hs[slot_new][lane] = sk;
           L.hy[slot_new][lane] = yk;
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          z.hcount = nw + 1;
+          // branch-free padded solves (entries past the history are zero)
+          double Rr[PF_HIST][PF_HIST], Yr[PF_HIST][PF_HIST], ri[PF_HIST], av[PF_HIST], bv[PF_HIST];
 #pragma unroll
-          for (int j = 0; j < PF_HIST; ++j) {
-            if (j < nw) {
-              // column nw of R and row/col nw of Y'Y (static j, runtime nw)
+          for (int i = 0; i < PF_HIST; ++i) {
+            ri[i] = L.rinv[i];
+            av[i] = L.av[i];
+            bv[i] = L.bv[i];
 #pragma unroll
-              for (int q = 0; q < PF_HIST; ++q) {
-                if (q == nw) {
-                  SYr[j][q] = r[4 + 2 * j];
-                  YYr[j][q] = r[5 + 2 * j];
-                  YYr[q][j] = r[5 + 2 * j];
-                }
-              }
-            }
+            for (int j = i; j < PF_HIST; ++j) { Rr[i][j] = L.Rm[i][j]; Yr[i][j] = L.YYm[i][j]; }
           }
-#pragma unroll
-          for (int q = 0; q < PF_HIST; ++q)
-            if (q == nw) { SYr[q][q] = r[2]; YYr[q][q] = r[3]; }
-          if (lane == 0) {
-#pragma unroll
-            for (int i = 0; i < PF_HIST; ++i)
-#pragma unroll
-              for (int j = 0; j < PF_HIST; ++j) { L.SY[i][j] = SYr[i][j]; L.YY[i][j] = YYr[i][j]; }
-          }
-          const int m = nw + 1;
-          z.hcount = m;
-          double av[PF_HIST], bv[PF_HIST], uu[PF_HIST], pp[PF_HIST];
-#pragma unroll
-          for (int j = 0; j < PF_HIST; ++j) {
-            av[j] = (j < nw) ? r[12 + 2 * j] : ((j == nw) ? r[20] : 0.0);
-            bv[j] = (j < nw) ? r[13 + 2 * j] : ((j == nw) ? r[21] : 0.0);
-            uu[j] = 0.0;
-            pp[j] = 0.0;
-          }
+          double uu[PF_HIST], pp[PF_HIST];
           // u = R^-1 a (back substitution)
 #pragma unroll
           for (int i = PF_HIST - 1; i >= 0; --i) {
-            if (i < m) {
-              double t = av[i];
+            double t = av[i];
 #pragma unroll
-              for (int j = i + 1; j < PF_HIST; ++j)
-                if (j < m) t -= SYr[i][j] * uu[j];
-              uu[i] = t / SYr[i][i];
-            }
+            for (int j = i + 1; j < PF_HIST; ++j) t = fma(-Rr[i][j], uu[j], t);
+            uu[i] = t * ri[i];
           }
           // w = (D + gamma Y'Y) u - gamma b ; p' = R^-T w (forward substitution)
 #pragma unroll
           for (int i = 0; i < PF_HIST; ++i) {
-            if (i < m) {
-              double w = SYr[i][i] * uu[i] - gam * bv[i];
+            double yu = 0.0;
 #pragma unroll
-              for (int j = 0; j < PF_HIST; ++j)
-                if (j < m) w += gam * YYr[i][j] * uu[j];
+            for (int j = 0; j < PF_HIST; ++j) yu = fma(j >= i ? Yr[i][j] : Yr[j][i], uu[j], yu);
+            double w = fma(Rr[i][i], uu[i], gam * (yu - bv[i]));
 #pragma unroll
-              for (int j = 0; j < PF_HIST; ++j)
-                if (j < i) w -= SYr[j][i] * pp[j];
-              pp[i] = w / SYr[i][i];
-            }
+            for (int j = 0; j < i; ++j) w = fma(-Rr[j][i], pp[j], w);
+            pp[i] = w * ri[i];
           }
           double Hg = gam * gq;
           double gHg = gam * gg;
 #pragma unroll
           for (int j = 0; j < PF_HIST; ++j) {
-            if (j < m) {
-              const int slot = pf_wrap(z.head + j, H);
-              Hg += pp[j] * L.hs[slot][lane] - gam * uu[j] * L.hy[slot][lane];
-              gHg += pp[j] * av[j] - gam * uu[j] * bv[j];
-            }
+            const int sl = pf_wrap(z.head + j, H);
+            Hg = fma(pp[j], L.hs[sl][lane], fma(-gam * uu[j], L.hy[sl][lane], Hg));
+            gHg = fma(pp[j], av[j], fma(-gam * uu[j], bv[j], gHg));
           }
           pk = -Hg;
           z.dfp_next = -gHg;
@@ -1075,14 +1158,22 @@ __device__ __forceinline__ bool lbfgs_step(const pf_fit_opts &o, LbLds &L, int &
 // State lives in LDS between evaluations; copy it into registers for the
 // step (one batch of independent LDS loads) and write it back at the end.
 __device__ __forceinline__ bool lbfgs_advance(const pf_fit_opts &o, LbLds &L, double &xq, double gq,
-                                              bool bad) {
+                                              double gpq, bool bad) {
   const int lane = pf_lane();
   PF_STAMP(6);
   LbScalars z = L.z;
-  int state = L.state;
+  int state = __builtin_amdgcn_readfirstlane(L.state);
+  // every scalar of the optimizer is wave-uniform: say so (SGPRs + scalar
+  // branches instead of exec-masked control flow)
+  {
+    static_assert(sizeof(LbScalars) % 4 == 0, "LbScalars words");
+    int *w = reinterpret_cast<int *>(&z);
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(LbScalars) / 4); ++i) w[i] = __builtin_amdgcn_readfirstlane(w[i]);
+  }
   double xk = L.xk[lane], gk = L.gk[lane], pk = L.pk[lane];
   PF_STAMP(7);
-  const bool need = lbfgs_step(o, L, state, z, xk, gk, pk, xq, gq, bad);
+  const bool need = lbfgs_step(o, L, state, z, xk, gk, pk, xq, gq, gpq, bad);
   PF_STAMP(8);
   L.xk[lane] = xk;
   L.gk[lane] = gk;
@@ -1103,7 +1194,7 @@ template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
 __global__ __launch_bounds__(NW * 64, 2) void k_fit(FitKArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   FitSmem<NW, KMAX, MODE> sm;
-  sm.carve(smem_raw, a.Tp, a.NB, a.P);
+  sm.carve(smem_raw, a.TQ, a.P);
   const int s = blockIdx.x, lane = pf_lane();
   const int P = a.P;
   double *th_out = a.theta + (size_t)s * P;
@@ -1128,26 +1219,34 @@ __global__ __launch_bounds__(NW * 64, 2) void k_fit(FitKArgs a) {
     if (lane == 0) memset(&L.z, 0, sizeof(LbScalars));
 #pragma unroll
     for (int q = 0; q < PF_HIST; ++q) { L.hs[q][lane] = 0.0; L.hy[q][lane] = 0.0; }
+    L.pk[lane] = 0.0;
+    if (lane < PF_HIST * PF_HIST) { (&L.Rm[0][0])[lane] = 0.0; (&L.YYm[0][0])[lane] = 0.0; }
+    if (lane < PF_HIST) { L.rinv[lane] = 0.0; L.av[lane] = 0.0; L.bv[lane] = 0.0; }
+    publish_theta<NW, KMAX, MODE>(a, sm, xq);
   }
   __syncthreads();
-  // ---- phase A: Stan-faithful L-BFGS (reverse communication)
+  // ---- phase A: Stan-faithful L-BFGS (reverse communication).  Per
+  // evaluation: row pass (all waves) | barrier | wave 0: assemble f, g ->
+  // optimizer step -> publish the next trial point | barrier.
   int n_eval = 0;
   while (true) {
-    double fq, gq;
-    const bool bad = eval_collective<NW, KMAX, O0, O1, O2, MODE>(a, sm, xq, fq, gq);
-    ++n_eval;
+    eval_rows<NW, KMAX, O0, O1, O2, MODE>(a, sm);
+    __syncthreads();
     if (pf_wave() == 0) {
+      double fq, gq, gpq;
+      const bool bad = eval_assemble<NW, KMAX, MODE>(a, sm, xq, L.pk[lane], fq, gq, gpq);
+      ++n_eval;
+      PF_STAMP(4);
       if (lane == 0) L.z.fq = fq;
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
-      const bool need = lbfgs_advance(a.o, L, xq, gq, bad);
-      if (lane == 0) L.need = need ? 1 : 0;
+      const bool need = lbfgs_advance(a.o, L, xq, gq, gpq, bad);
+      if (need) publish_theta<NW, KMAX, MODE>(a, sm, xq);
+      if (lane == 0) sm.flag[0] = need ? 1 : 0;
     }
     __syncthreads();
-    const int need = L.need;
-    __syncthreads();
     PF_STAMP(5);
-    if (!need) break;
+    if (!__builtin_amdgcn_readfirstlane(sm.flag[0])) break;
   }
   double xk = L.xk[lane];
   double gk = L.gk[lane];
@@ -1176,7 +1275,7 @@ template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
 __global__ __launch_bounds__(NW * 64, 2) void k_polish(FitKArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   FitSmem<NW, KMAX, MODE> sm;
-  sm.carve(smem_raw, a.Tp, a.NB, a.P);
+  sm.carve(smem_raw, a.TQ, a.P);
   const int s = blockIdx.x, lane = pf_lane();
   const int P = a.P;
   const int st = a.status[s];
@@ -1735,7 +1834,33 @@ int pf_prepare(pf_ctx *ctx, int n_series, const pf_grid *grid, int growth, const
 
 }  // extern "C"
 
+// ---------------------------------------------------------------- lane-blocked grid
+// Position q = r*NL + L of the copy holds natural row i = L*R + r (rows past
+// T: t = 0, X = 0, seg = S, no changepoint starts).  Built per fit call into
+// the context workspace (K+1 doubles + 1 int per position; ~0.4 MB at 1826
+// days), read by every series of the batch.
+__global__ __launch_bounds__(256) void k_permute_grid(const double *__restrict__ t,
+                                                      const int32_t *__restrict__ seg,
+                                                      const double *__restrict__ XT, int T, int Tp,
+                                                      int K, int S, int R, int NL,
+                                                      double *__restrict__ tP,
+                                                      int32_t *__restrict__ sgP,
+                                                      double *__restrict__ XTP) {
+  const int TQ = NL * R;
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  if (q >= TQ) return;
+  const int r = q / NL, L = q - r * NL;
+  const int i = L * R + r;
+  const bool v = i < T;
+  tP[q] = v ? t[i] : 0.0;
+  const int sg = v ? seg[i] : S;
+  const int sp = v ? (i > 0 ? seg[i - 1] : 0) : S;
+  sgP[q] = sg | ((sg - sp) << 16);
+  for (int f = 0; f < K; ++f) XTP[(size_t)f * TQ + q] = v ? XT[(size_t)f * Tp + i] : 0.0;
+}
+
 // ---------------------------------------------------------------- dispatch
+#define PF_FIT_NW 4
 namespace {
 
 FitKArgs make_fit_args(const pf_problem *pb) {
@@ -1748,6 +1873,8 @@ FitKArgs make_fit_args(const pf_problem *pb) {
   a.growth = pb->growth;
   a.P = 3 + a.S + a.K;
   a.NB = a.Tp / 64;
+  a.R = (a.T + PF_FIT_NW * 64 - 1) / (PF_FIT_NW * 64);
+  a.TQ = PF_FIT_NW * 64 * a.R;
   a.t = pb->grid.t;
   a.XT = pb->grid.XT;
   a.t_change = pb->grid.t_change;
@@ -1762,8 +1889,9 @@ FitKArgs make_fit_args(const pf_problem *pb) {
 
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
 int launch_fitlike(pf_ctx *ctx, bool fit, const FitKArgs &a, int n, hipStream_t st) {
-  const size_t smem = FitSmem<NW, KMAX, MODE>::bytes(a.Tp, a.NB, a.P);
-  if (smem > 160 * 1024) return set_err(ctx, "fit: series too long for the LDS budget");
+  const size_t smem = FitSmem<NW, KMAX, MODE>::bytes(a.TQ, a.P, false);
+  const size_t smem_p = FitSmem<NW, KMAX, MODE>::bytes(a.TQ, a.P, true);
+  if (smem_p > 160 * 1024) return set_err(ctx, "fit: series too long for the LDS budget");
   if (fit) {
     auto kern = k_fit<NW, KMAX, O0, O1, O2, MODE>;
     PF_HIP(ctx, hipFuncSetAttribute((const void *)kern,
@@ -1773,8 +1901,8 @@ int launch_fitlike(pf_ctx *ctx, bool fit, const FitKArgs &a, int n, hipStream_t 
     if (a.o.polish && a.ws && a.growth == PF_GROWTH_LINEAR && a.K <= 32 && 2 + a.S <= 32) {
       auto kp = k_polish<NW, KMAX, O0, O1, O2, MODE>;
       PF_HIP(ctx, hipFuncSetAttribute((const void *)kp,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
-      PF_TIMED_LAUNCH(ctx, "k_polish", n, st, kp, dim3(n), dim3(NW * 64), smem, st, a);
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem_p));
+      PF_TIMED_LAUNCH(ctx, "k_polish", n, st, kp, dim3(n), dim3(NW * 64), smem_p, st, a);
     }
   } else {
     auto kern = k_objgrad<NW, KMAX, O0, O1, O2, MODE>;
@@ -1794,18 +1922,42 @@ int launch_fitlike(pf_ctx *ctx, bool fit, const FitKArgs &a, int n, hipStream_t 
 int dispatch_fitlike(pf_ctx *ctx, bool fit, const FitKArgs &a, int n, int fourier103, int mode,
                      hipStream_t st) {
   if (fourier103 && a.K == 26) {
-    if (mode == MODE_MULT) return launch_fitlike<4, 26, 10, 3, 0, MODE_MULT>(ctx, fit, a, n, st);
-    if (mode == MODE_ADD) return launch_fitlike<4, 26, 10, 3, 0, MODE_ADD>(ctx, fit, a, n, st);
-    return launch_fitlike<4, 26, 10, 3, 0, MODE_MIXED>(ctx, fit, a, n, st);
+    if (mode == MODE_MULT) return launch_fitlike<PF_FIT_NW, 26, 10, 3, 0, MODE_MULT>(ctx, fit, a, n, st);
+    if (mode == MODE_ADD) return launch_fitlike<PF_FIT_NW, 26, 10, 3, 0, MODE_ADD>(ctx, fit, a, n, st);
+    return launch_fitlike<PF_FIT_NW, 26, 10, 3, 0, MODE_MIXED>(ctx, fit, a, n, st);
   }
-  if (a.K <= 32) return launch_fitlike<4, 32, 0, 0, 0, MODE_MIXED>(ctx, fit, a, n, st);
-  if (a.K <= 61) return launch_fitlike<4, 61, 0, 0, 0, MODE_MIXED>(ctx, fit, a, n, st);
+  if (a.K <= 32) return launch_fitlike<PF_FIT_NW, 32, 0, 0, 0, MODE_MIXED>(ctx, fit, a, n, st);
+  if (a.K <= 61) return launch_fitlike<PF_FIT_NW, 61, 0, 0, 0, MODE_MIXED>(ctx, fit, a, n, st);
   return set_err(ctx, "fit: K > 61 not supported");
 }
 
 }  // namespace
 
 extern "C" {
+
+// Context scratch for one fit-like call: [lane-blocked grid | polish rows],
+// then the permutation launch (stream-ordered with the fit that reads it).
+static int prepare_fit_scratch(pf_ctx *ctx, FitKArgs &a, int n_series, bool polish, hipStream_t st) {
+  const size_t TQ = (size_t)a.TQ;
+  size_t gbytes = TQ * sizeof(double) * (1 + (size_t)a.K) + TQ * sizeof(int32_t);
+  gbytes = (gbytes + 255) & ~(size_t)255;
+  const size_t pbytes = polish ? (size_t)n_series * 3 * a.Tp * sizeof(double) : 0;
+  void *w = nullptr;
+  const int rc = ctx_workspace(ctx, gbytes + pbytes, &w);
+  if (rc) return rc;
+  double *base = (double *)w;
+  a.tP = base;
+  a.XTP = base + TQ;
+  a.sgP = (int32_t *)(base + TQ * (1 + (size_t)a.K));
+  a.ws = polish ? (double *)((char *)w + gbytes) : nullptr;
+  const int nb = (int)((TQ + 255) / 256);
+  PF_TIMED_LAUNCH(ctx, "k_permute_grid", nb, st, k_permute_grid, dim3(nb), dim3(256), 0, st,
+                  a.t, a.seg, a.XT, a.T, a.Tp, a.K, a.S, a.R, PF_FIT_NW * 64,
+                  const_cast<double *>(a.tP), const_cast<int32_t *>(a.sgP),
+                  const_cast<double *>(a.XTP));
+  PF_HIP(ctx, hipGetLastError());
+  return 0;
+}
 
 static int is_fourier103(const pf_problem *pb) {
   return pb->fourier_orders[0] == 10 && pb->fourier_orders[1] == 3 && pb->fourier_orders[2] == 0;
@@ -1836,6 +1988,8 @@ int pf_objective_grad(pf_ctx *ctx, const pf_problem *pb, const double *theta, do
   a.theta = const_cast<double *>(theta);
   a.f_out = f;
   a.g_out = g;
+  rc = prepare_fit_scratch(ctx, a, pb->n_series, false, (hipStream_t)stream);
+  if (rc) return rc;
   return dispatch_fitlike(ctx, false, a, pb->n_series, is_fourier103(pb), mode_of(pb),
                           (hipStream_t)stream);
 }
@@ -1856,13 +2010,8 @@ int pf_fit(pf_ctx *ctx, const pf_problem *pb, const pf_fit_opts *opts, double *t
   a.n_iter = n_iter;
   a.n_eval = n_eval;
   a.o = *opts;
-  a.ws = nullptr;
-  if (opts->polish) {
-    void *w = nullptr;
-    const int rc2 = ctx_workspace(ctx, (size_t)pb->n_series * 3 * pb->grid.T_pad * sizeof(double), &w);
-    if (rc2) return rc2;
-    a.ws = (double *)w;
-  }
+  rc = prepare_fit_scratch(ctx, a, pb->n_series, opts->polish != 0, (hipStream_t)stream);
+  if (rc) return rc;
   return dispatch_fitlike(ctx, true, a, pb->n_series, is_fourier103(pb), mode_of(pb),
                           (hipStream_t)stream);
 }

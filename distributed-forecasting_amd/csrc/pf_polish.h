@@ -49,13 +49,15 @@ __device__ __forceinline__ void hessian_collective(const FitKArgs &a, FitSmem<NW
   double Q = 0.0;
   const double th_m = sm.th[1];
   const bool linear = (a.growth == PF_GROWTH_LINEAR);
-  for (int b = wave; b < a.NB; b += NW) {
-    const int i = b * 64 + lane;
+  constexpr int NL = NW * 64;
+  for (int rr = 0; rr < a.R; ++rr) {
+    const int q = rr * NL + threadIdx.x;        // lane-blocked position
+    const int i = threadIdx.x * a.R + rr;       // natural row
     const bool valid = i < T;
     RowIn cur;
-    load_row<O0, O1, O2>(a.t, a.seg, a.XT, Tp, i, cur);
+    load_rowp<O0, O1, O2>(a, q, cur);
     double xf[KMAX];
-    row_features_from<KMAX, O0, O1, O2>(cur, a.XT, Tp, K, i, xf);
+    row_features_from<KMAX, O0, O1, O2>(cur, a.XTP, a.TQ, K, q, xf);
     double xm[4] = {0.0, 0.0, 0.0, 0.0}, xa[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int f2 = 0; f2 < KMAX; ++f2) {
@@ -67,11 +69,13 @@ __device__ __forceinline__ void hessian_collective(const FitKArgs &a, FitSmem<NW
     const double xba = (xa[0] + xa[1]) + (xa[2] + xa[3]);
     const double tr = linear ? fma(sm.kseg[cur.seg], cur.t, sm.mseg[cur.seg]) : th_m;
     const double u = 1.0 + xbm;
-    const double r = valid ? (sm.y[i] - fma(tr, u, xba)) : 0.0;
+    const double r = valid ? (sm.y[q] - fma(tr, u, xba)) : 0.0;
     Q = fma(r, r, Q);
-    ws[i] = valid ? u : 0.0;
-    ws[Tp + i] = valid ? tr : 0.0;
-    ws[2 * Tp + i] = r;
+    if (i < Tp) {
+      ws[i] = valid ? u : 0.0;
+      ws[Tp + i] = valid ? tr : 0.0;
+      ws[2 * Tp + i] = r;
+    }
   }
   Q = wave_sum(Q);
   if (lane == 0) sm.rrw[wave] = Q;
