@@ -14,7 +14,8 @@ LIB_PATH = os.path.join(_HERE, "libprophet_hip.so")
 
 PF_GROWTH = {"linear": 0, "logistic": 1, "flat": 2}
 STATUS_NAMES = {0: "SUCCESS", 10: "ABSX", 20: "ABSF", 21: "RELF", 30: "ABSGRAD",
-                31: "RELGRAD", 40: "MAXIT", -1: "LSFAIL", -2: "BADINIT", 50: "CONSTANT"}
+                31: "RELGRAD", 40: "MAXIT", -1: "LSFAIL", -2: "BADINIT", 50: "CONSTANT",
+                60: "WARMUP", 70: "MAP"}
 PF_ST_CONSTANT = 50
 
 # Every symbol include/prophet_hip.h declares (checked by tests/test_abi.py).
@@ -53,7 +54,8 @@ class PfFitOpts(ctypes.Structure):
     _fields_ = [("init_alpha", ctypes.c_double), ("tol_obj", ctypes.c_double),
                 ("tol_rel_obj", ctypes.c_double), ("tol_grad", ctypes.c_double),
                 ("tol_rel_grad", ctypes.c_double), ("tol_param", ctypes.c_double),
-                ("max_iter", i32), ("history", i32), ("polish", i32), ("polish_max_iter", i32)]
+                ("max_iter", i32), ("history", i32), ("polish", i32), ("polish_max_iter", i32),
+                ("lbfgs_warmup", i32), ("_pad", i32)]
 
 
 class PfPredictArgs(ctypes.Structure):

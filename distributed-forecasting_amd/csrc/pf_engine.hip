@@ -289,6 +289,8 @@ struct FitKArgs {
   double *f_out, *f_stan, *g_out;
   int32_t *status, *n_iter, *n_eval;
   pf_fit_opts o;
+  int pass;      // 0: first L-BFGS pass; >0: resume series the polish did not certify
+  int warm_cap;  // this pass's iteration cap is the warm-up cap (MAXIT -> WARMUP)
 };
 
 // Generated Fourier block: harmonics r >= 1 from the first harmonic column
@@ -1199,7 +1201,10 @@ __global__ __launch_bounds__(NW * 64, 2) void k_fit(FitKArgs a) {
   const int P = a.P;
   double *th_out = a.theta + (size_t)s * P;
   const int st_in = a.status[s];
-  if (st_in == PF_ST_CONSTANT) {
+  if (a.pass > 0) {
+    // resume pass: only series whose polish did not certify the MAP
+    if (st_in == PF_ST_CONSTANT || st_in == PF_ST_BADINIT || st_in == PF_ST_MAP) return;
+  } else if (st_in == PF_ST_CONSTANT) {
     // Prophet: params = init, sigma_obs = 1e-9; optimizer skipped
     if (threadIdx.x == 0) {
       th_out[2 + a.S] = log(1e-9);
@@ -1252,17 +1257,22 @@ __global__ __launch_bounds__(NW * 64, 2) void k_fit(FitKArgs a) {
   double gk = L.gk[lane];
   double f = L.z.fk;
   const double f_stan = f;
-  const int st_stan = L.z.ret, it_stan = L.z.itNum;
-  int n_newton = 0;
-  (void)n_newton;
+  int st_stan = L.z.ret;
+  const int it_stan = L.z.itNum;
+  if (a.warm_cap && st_stan == PF_ST_MAXIT) st_stan = PF_ST_WARMUP;
   if (threadIdx.x < 64) {
     if (lane < P) th_out[lane] = xk;
     if (lane == 0) {
       a.f_out[s] = f;
-      a.f_stan[s] = f_stan;
+      if (a.pass == 0) {
+        a.f_stan[s] = f_stan;
+        a.n_iter[s] = it_stan;
+        a.n_eval[s] = n_eval;
+      } else {
+        a.n_iter[s] += it_stan;
+        a.n_eval[s] += n_eval;
+      }
       a.status[s] = st_stan;
-      a.n_iter[s] = it_stan;
-      a.n_eval[s] = n_eval;
     }
   }
 }
@@ -1279,7 +1289,7 @@ __global__ __launch_bounds__(NW * 64, 2) void k_polish(FitKArgs a) {
   const int s = blockIdx.x, lane = pf_lane();
   const int P = a.P;
   const int st = a.status[s];
-  if (st == PF_ST_CONSTANT || st == PF_ST_BADINIT) return;
+  if (st == PF_ST_CONSTANT || st == PF_ST_BADINIT || st == PF_ST_MAP) return;
   double *th_out = a.theta + (size_t)s * P;
   load_y<NW, KMAX, MODE>(a, sm, s);
   double x = (lane < P) ? th_out[lane] : 0.0;
@@ -1288,12 +1298,13 @@ __global__ __launch_bounds__(NW * 64, 2) void k_polish(FitKArgs a) {
   const bool bad = eval_collective<NW, KMAX, O0, O1, O2, MODE>(a, sm, x, f, g);
   if (bad) return;
   int n_eval = 1, n_newton = 0;
-  polish_run<NW, KMAX, O0, O1, O2, MODE>(a, sm, x, f, g, n_eval, n_newton);
+  const bool cert = polish_run<NW, KMAX, O0, O1, O2, MODE>(a, sm, x, f, g, n_eval, n_newton);
   if (threadIdx.x < 64) {
     if (lane < P) th_out[lane] = x;
     if (lane == 0) {
       a.f_out[s] = f;
       a.n_eval[s] += n_eval;
+      if (cert) a.status[s] = PF_ST_MAP;
     }
   }
 }
@@ -1768,6 +1779,8 @@ void pf_default_fit_opts(pf_fit_opts *o) {
   o->history = 5;
   o->polish = 1;
   o->polish_max_iter = 20;
+  o->lbfgs_warmup = 60;
+  o->_pad = 0;
 }
 
 int pf_num_changepoints(int T, int n_changepoints, double changepoint_range) {
@@ -1894,15 +1907,37 @@ int launch_fitlike(pf_ctx *ctx, bool fit, const FitKArgs &a, int n, hipStream_t 
   if (smem_p > 160 * 1024) return set_err(ctx, "fit: series too long for the LDS budget");
   if (fit) {
     auto kern = k_fit<NW, KMAX, O0, O1, O2, MODE>;
+    auto kp = k_polish<NW, KMAX, O0, O1, O2, MODE>;
     PF_HIP(ctx, hipFuncSetAttribute((const void *)kern,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
-    PF_TIMED_LAUNCH(ctx, "k_fit", n, st, kern, dim3(n), dim3(NW * 64), smem, st, a);
-    PF_HIP(ctx, hipGetLastError());
-    if (a.o.polish && a.ws && a.growth == PF_GROWTH_LINEAR && a.K <= 32 && 2 + a.S <= 32) {
-      auto kp = k_polish<NW, KMAX, O0, O1, O2, MODE>;
-      PF_HIP(ctx, hipFuncSetAttribute((const void *)kp,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem_p));
-      PF_TIMED_LAUNCH(ctx, "k_polish", n, st, kp, dim3(n), dim3(NW * 64), smem_p, st, a);
+    PF_HIP(ctx, hipFuncSetAttribute((const void *)kp,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem_p));
+    const bool polish = a.o.polish && a.ws && a.growth == PF_GROWTH_LINEAR && a.K <= 32 && 2 + a.S <= 32;
+    const int W = a.o.lbfgs_warmup;
+    // passes: (cap, warm?) — warm-up, one more warm-up for uncertified
+    // series, then Stan's full rules; each followed by the polish
+    int caps[3], warm[3], npass = 1;
+    if (polish && W > 0 && W < a.o.max_iter) {
+      caps[0] = W; warm[0] = 1;
+      caps[1] = W; warm[1] = 1;
+      caps[2] = a.o.max_iter; warm[2] = 0;
+      npass = 3;
+    } else {
+      caps[0] = a.o.max_iter; warm[0] = 0;
+    }
+    for (int ps = 0; ps < npass; ++ps) {
+      FitKArgs b = a;
+      b.o.max_iter = caps[ps];
+      b.warm_cap = warm[ps];
+      b.pass = ps;
+      PF_TIMED_LAUNCH(ctx, ps == 0 ? "k_fit" : "k_fit_resume", n, st, kern, dim3(n), dim3(NW * 64),
+                      smem, st, b);
+      PF_HIP(ctx, hipGetLastError());
+      if (polish) {
+        PF_TIMED_LAUNCH(ctx, ps == 0 ? "k_polish" : "k_polish_resume", n, st, kp, dim3(n),
+                        dim3(NW * 64), smem_p, st, b);
+        PF_HIP(ctx, hipGetLastError());
+      }
     }
   } else {
     auto kern = k_objgrad<NW, KMAX, O0, O1, O2, MODE>;

@@ -332,11 +332,13 @@ __device__ __forceinline__ bool qp_active(const FitKArgs &a, FitSmem<NW, KMAX, M
     const int jadd = __ffsll((long long)hit) - 1;
     if (lane == jadd) { zero = false; sgn_ = -((gq > 0.0) - (gq < 0.0)); }
   }
-  return true;
+  return false;  // active set did not settle
 }
 
+// Returns true when the polish certifies the optimum: the last lasso-QP
+// (exact Hessian, solved to KKT) predicts no decrease beyond 1e-15 |f|.
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
-__device__ __forceinline__ void polish_run(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, double &x, double &f,
+__device__ __forceinline__ bool polish_run(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, double &x, double &f,
                            double &g, int &n_eval, int &n_newton) {
   const int lane = pf_lane(), wave = pf_wave();
   const int S = a.S;
@@ -344,6 +346,7 @@ __device__ __forceinline__ void polish_run(const FitKArgs &a, FitSmem<NW, KMAX, 
   const bool isd = (lane >= 2 && lane < 2 + S);
   double *ws = a.ws + (size_t)blockIdx.x * 3 * a.Tp;
   n_newton = 0;
+  bool cert = false;
   for (int it = 0; it < a.o.polish_max_iter; ++it) {
     const double gh = isd ? g - c * (double)((x > 0.0) - (x < 0.0)) : g;
     hessian_collective<NW, KMAX, O0, O1, O2, MODE>(a, sm, x, gh, ws);
@@ -360,9 +363,13 @@ __device__ __forceinline__ void polish_run(const FitKArgs &a, FitSmem<NW, KMAX, 
     }
     __syncthreads();
     const double dec = sm.fout[2];
+    const bool qp_ok = sm.fout[3] != 0.0;
     const double d = sm.pd[lane];
     __syncthreads();
-    if (!(dec < -1e-15 * fabs(f))) break;
+    if (!(dec < -1e-15 * fabs(f))) {
+      cert = qp_ok && dec == dec;
+      break;
+    }
     ++n_newton;
     double alpha = 1.0, fn = 0.0, gn = 0.0, xn = x;
     bool acc = false;
@@ -378,4 +385,5 @@ __device__ __forceinline__ void polish_run(const FitKArgs &a, FitSmem<NW, KMAX, 
     f = fn;
     g = gn;
   }
+  return cert;
 }

@@ -305,16 +305,28 @@ class Engine:
         self.ctx.check(rc, "pf_objective_grad")
         return f, g
 
-    def fit_opts(self, polish: bool = True, **over) -> L.PfFitOpts:
+    def fit_opts(self, polish: bool = True, stan_faithful: bool = False, **over) -> L.PfFitOpts:
+        """pf_fit_opts: Stan optimizing() defaults + the engine's polish.
+        ``stan_faithful`` runs Stan's full L-BFGS termination rules before the
+        polish (lbfgs_warmup = 0) instead of the warm-up hand-off."""
         o = L.PfFitOpts()
         self.ctx.lib.pf_default_fit_opts(ctypes.byref(o))
         o.polish = 1 if polish else 0
+        if stan_faithful:
+            o.lbfgs_warmup = 0
         for k, v in over.items():
             setattr(o, k, v)
         return o
 
-    def fit(self, grid: DeviceGrid, Y: torch.Tensor, polish: bool = True, **opt) -> FitResult:
-        """Fit every row of Y [n, T_pad] (raw y, float64, on this GPU)."""
+    def fit(self, grid: DeviceGrid, Y: torch.Tensor, polish: bool = True,
+            stan_faithful: bool = False, **opt) -> FitResult:
+        """Fit every row of Y [n, T_pad] (raw y, float64, on this GPU).
+
+        Default: Stan L-BFGS warm-up (<= lbfgs_warmup iterations) handed to
+        the exact-MAP polish (status PF_ST_MAP when certified; uncertified
+        series resume L-BFGS).  ``stan_faithful=True`` first runs Stan's full
+        termination rules (the reference's optimizer run), then polishes to
+        the same MAP; ``polish=False`` stops where Stan stops."""
         n = Y.shape[0]
         y_scale, y_scaled, theta, status = self.prepare(grid, Y)
         dev = Y.device
@@ -323,7 +335,7 @@ class Engine:
         n_iter = torch.empty(n, dtype=torch.int32, device=dev)
         n_eval = torch.empty(n, dtype=torch.int32, device=dev)
         pb = self.problem(grid, y_scaled, n)
-        o = self.fit_opts(polish, **opt)
+        o = self.fit_opts(polish, stan_faithful, **opt)
         rc = self.ctx.lib.pf_fit(self.ctx.h, ctypes.byref(pb), ctypes.byref(o), _ptr(theta),
                                  _ptr(f), _ptr(f_stan), _ptr(status), _ptr(n_iter), _ptr(n_eval),
                                  _stream(self.device))

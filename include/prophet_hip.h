@@ -42,7 +42,9 @@ enum pf_status {
   PF_ST_SUCCESS = 0, PF_ST_ABSX = 10, PF_ST_ABSF = 20, PF_ST_RELF = 21,
   PF_ST_ABSGRAD = 30, PF_ST_RELGRAD = 31, PF_ST_MAXIT = 40,
   PF_ST_LSFAIL = -1, PF_ST_BADINIT = -2,
-  PF_ST_CONSTANT = 50          /* min y == max y: optimizer skipped (Prophet rule) */
+  PF_ST_CONSTANT = 50,         /* min y == max y: optimizer skipped (Prophet rule) */
+  PF_ST_WARMUP = 60,           /* L-BFGS stopped at the warm-up cap (lbfgs_warmup)  */
+  PF_ST_MAP = 70               /* exact-MAP polish certified the optimum            */
 };
 
 /* One Fourier seasonality block: columns sin/cos(2π(i+1)d/period), i<order. */
@@ -89,6 +91,14 @@ typedef struct {
   int32_t max_iter, history;
   /* engine: exact-MAP proximal-Newton polish after the Stan phase (0/1) */
   int32_t polish, polish_max_iter;
+  /* engine: with polish, the Stan L-BFGS phase runs at most lbfgs_warmup
+   * iterations before the polish takes it to the MAP (Stan's zig-zag at the
+   * |delta| kink adds hundreds of evaluations that do not move the MAP); a
+   * series whose polish does not certify convergence resumes L-BFGS (once
+   * more for lbfgs_warmup iterations, then with Stan's full termination
+   * rules) and is polished again.  0 = run Stan's full termination rules
+   * first (the reference's behaviour), then polish.                        */
+  int32_t lbfgs_warmup, _pad;
 } pf_fit_opts;
 
 /* ---------------------------------------------------------------- context */
@@ -146,8 +156,11 @@ int pf_objective_grad(pf_ctx *ctx, const pf_problem *pb, const double *theta,
 
 /* -------------------------------------------------- K3: batched fit (MAP)
  * theta_inout[n*P]: init in, optimum out.  f_out[n] final -log posterior,
- * f_stan[n] objective where the Stan-faithful phase stopped, status[n]
- * (in: PF_ST_CONSTANT rows are skipped), n_iter[n], n_eval[n].           */
+ * f_stan[n] objective where the (first) L-BFGS phase stopped, status[n]
+ * (in: PF_ST_CONSTANT rows are skipped; out: PF_ST_MAP when the polish
+ * certified the optimum, else the Stan termination code), n_iter[n]
+ * (L-BFGS iterations), n_eval[n] (objective+gradient evaluations, all
+ * phases).  Scratch is stream-ordered in the context.                    */
 int pf_fit(pf_ctx *ctx, const pf_problem *pb, const pf_fit_opts *opts,
            double *theta_inout, double *f_out, double *f_stan,
            int32_t *status, int32_t *n_iter, int32_t *n_eval, void *stream);
