@@ -58,8 +58,13 @@ __device__ unsigned long long pf_dbg[32];
     if (blockIdx.x == 0 && threadIdx.x == 0)                                     \
       atomicAdd(&pf_dbg[i], (unsigned long long)__builtin_amdgcn_s_memtime());   \
   } while (0)
+#define PF_COUNT(i)                                                              \
+  do {                                                                           \
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&pf_dbg[i], 1ull);        \
+  } while (0)
 #else
 #define PF_STAMP(i) do { } while (0)
+#define PF_COUNT(i) do { } while (0)
 #endif
 
 static int set_err(pf_ctx *ctx, const char *msg) {

@@ -91,12 +91,29 @@ __device__ __forceinline__ void hessian_collective(const FitKArgs &a, FitSmem<NW
   const bool f2v = c16 < K, f3v = c1 < K;
   const double cm2 = f2v ? a.s_m[c16] : 0.0, ca2 = f2v ? a.s_a[c16] : 0.0;
   const double cm3 = f3v ? a.s_m[c1] : 0.0, ca3 = f3v ? a.s_a[c1] : 0.0;
-  const int nks = Tp >> 2;
+  const int nks = (T + 3) >> 2;  // k-steps holding a valid row
+  // operands of the next k-step are loaded before this step's MFMAs
+  // (global/L2 latency would otherwise stall every step)
+  struct HIn { double u, tr, r, ti, X2, X3; int sg; };
+  auto hload = [&](int s_, HIn &h) {
+    const int rho = 4 * s_ + (lane >> 4);
+    h.u = ws[rho];
+    h.tr = ws[Tp + rho];
+    h.r = ws[2 * Tp + rho];
+    h.ti = a.t[rho];
+    h.sg = a.seg[rho];
+    h.X2 = f2v ? a.XT[(size_t)c16 * Tp + rho] : 0.0;
+    h.X3 = f3v ? a.XT[(size_t)c1 * Tp + rho] : 0.0;
+  };
+  HIn nx;
+  if (wave < nks) hload(wave, nx);
   for (int s = wave; s < nks; s += NW) {
+    const HIn cu = nx;
+    if (s + NW < nks) hload(s + NW, nx);
     const int rho = 4 * s + (lane >> 4);
-    const double u = ws[rho], tr = ws[Tp + rho], r = ws[2 * Tp + rho];
-    const double ti = a.t[rho];
-    const int sg = a.seg[rho];
+    const double u = cu.u, tr = cu.tr, r = cu.r;
+    const double ti = cu.ti;
+    const int sg = cu.sg;
     // a columns (tile 0: c16, tile 1: 16 + c16)
     double D0, D1;
     if (c16 == 0) D0 = ti;
@@ -106,8 +123,7 @@ __device__ __forceinline__ void hessian_collective(const FitKArgs &a, FitSmem<NW
     if (rho >= T) { D0 = 0.0; D1 = 0.0; }
     const double Du0 = D0 * u, Du1 = D1 * u;
     // beta columns (tile 2: f = c16, tile 3: f = 16 + c16)
-    const double X2 = f2v ? a.XT[(size_t)c16 * Tp + rho] : 0.0;
-    const double X3 = f3v ? a.XT[(size_t)c1 * Tp + rho] : 0.0;
+    const double X2 = cu.X2, X3 = cu.X3;
     const double k2 = fma(tr, cm2, ca2), k3 = fma(tr, cm3, ca3);
     const double V2 = X2 * k2, V3 = X3 * k3;
     const double W2 = X2 * fma(u, k2, -r * cm2), W3 = X3 * fma(u, k3, -r * cm3);
@@ -195,53 +211,134 @@ __device__ __forceinline__ void hessian_collective(const FitKArgs &a, FitSmem<NW
   }
 }
 
-// Cholesky (right-looking, lane = column of the trailing square) + solve,
-// wave-local.  M (n x n, stride LD) overwritten by L; b (lane i = b_i) -> x.
-__device__ __forceinline__ bool wave_chol_solve(double *M, int LD, int n, double &b) {
-  const int lane = pf_lane();
-  for (int k = 0; k < n; ++k) {
-    const double d = M[k * LD + k];
-    if (!(d > 0.0)) return false;
-    const double Lkk = sqrt(d);
-    double Ljk = 0.0;
-    if (lane > k && lane < n) {
-      Ljk = M[lane * LD + k] / Lkk;
-      M[lane * LD + k] = Ljk;
+// Symmetric sweep operator on A (P x P, stride LD, LDS; wave-local, lane =
+// column j).  Sweeping k in (rev = false) or out (rev = true) with pivot
+// d = A[k][k]:  A[i][j] -= A[i][k] A[k][j] / d  (i, j != k),
+//               A[i][k] = A[k][i] = +-A[i][k] / d,  A[k][k] = -1/d.
+// After sweeping the set F, A_FF = -(H_FF)^-1, A_FZ = (H_FF)^-1 H_FZ and
+// A_ZZ is the Schur complement, so each active-set change costs one O(P^2)
+// sweep instead of a refactorisation.  A sweep-in needs d > 0 (H_FF PD).
+__device__ __forceinline__ bool wave_sweep(double *A, int LD, int P, int k, bool rev) {
+  const int j = pf_lane();
+  const double d = A[k * LD + k];
+  if (!rev && !(d > 0.0)) return false;
+  if (rev && !(d < 0.0)) return false;
+  const double inv = 1.0 / d;
+  const double akj = (j < P) ? A[k * LD + j] : 0.0;
+  const double sj = akj * inv;
+  // row k (= column k) is held across lanes in akj: A[k][i] = readlane(akj, i).
+  // Rows in blocks of 8, all loads of a block before its stores; every
+  // per-row condition is uniform (lane k's own column is rewritten below).
+  if (j < P) {
+    for (int i0 = 0; i0 < P; i0 += 8) {
+      double av[8], ak[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int i = i0 + q;
+        if (i < P) {
+          ak[q] = readlane_f64(akj, i);
+          av[q] = A[i * LD + j];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int i = i0 + q;
+        if (i < P && i != k) A[i * LD + j] = fma(-ak[q], sj, av[q]);
+      }
     }
-    if (lane == k) M[k * LD + k] = Lkk;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    if (lane > k && lane < n) {
-      for (int i = k + 1; i < n; ++i) M[i * LD + lane] -= M[i * LD + k] * Ljk;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
   }
-  // forward: L y = b
-  for (int k = 0; k < n; ++k) {
-    const double yk = readlane_f64(b, k) / M[k * LD + k];
-    if (lane == k) b = yk;
-    if (lane > k && lane < n) b -= M[lane * LD + k] * yk;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  if (j < P && j != k) {
+    const double v = rev ? -sj : sj;
+    A[k * LD + j] = v;
+    A[j * LD + k] = v;
   }
-  // backward: L^T x = y
-  for (int k = n - 1; k >= 0; --k) {
-    const double xk = readlane_f64(b, k) / M[k * LD + k];
-    if (lane == k) b = xk;
-    if (lane < k) b -= M[k * LD + lane] * xk;
-  }
+  if (j == k) A[k * LD + k] = -inv;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
   return true;
 }
 
+// Workgroup version of the initial sweep-in: A = H, then sweep every
+// coordinate free under the QP's starting active set (|gh| > c for delta,
+// always for the rest).  Rows are split across the NW waves (lane =
+// column); two barriers per sweep.  Every wave derives the same free set
+// from its own copy of x and gh (lane = parameter).  flag[1] = 1 on a
+// non-positive pivot.
+template <int NW, int KMAX, int MODE>
+__device__ __forceinline__ void sweep_in_free(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, double gh,
+                                              double c) {
+  const int lane = pf_lane(), wave = pf_wave();
+  const int P = a.P, S = a.S, LD = sm.LD;
+  const double *H = sm.U;
+  double *A = sm.U + (size_t)P * LD;
+  constexpr int RW = (64 + NW - 1) / NW;  // rows per wave
+  const int r0 = wave * RW;
+  if (lane < P)
+    for (int i = r0; i < r0 + RW && i < P; ++i) A[i * LD + lane] = H[i * LD + lane];
+  if (threadIdx.x == 0) sm.flag[1] = 0;
+  __syncthreads();
+  const bool isd = (lane >= 2 && lane < 2 + S);
+  const bool zero = isd && fabs(gh) <= c;
+  unsigned long long fm = __ballot(lane < P && !zero);
+  while (fm) {
+    const int k = __ffsll((long long)fm) - 1;
+    fm &= fm - 1;
+    const double d = A[k * LD + k];
+    if (!(d > 0.0)) {  // uniform across the workgroup
+      if (threadIdx.x == 0) sm.flag[1] = 1;
+      break;
+    }
+    const double inv = 1.0 / d;
+    const double akj = (lane < P) ? A[k * LD + lane] : 0.0;
+    const double sj = akj * inv;
+    if (lane < P) {
+#pragma unroll
+      for (int q = 0; q < RW; ++q) {
+        const int i = r0 + q;
+        if (i < P && i != k) A[i * LD + lane] = fma(-readlane_f64(akj, i), sj, A[i * LD + lane]);
+      }
+    }
+    __syncthreads();
+    if (wave == 0) {
+      if (lane < P && lane != k) {
+        A[k * LD + lane] = sj;
+        A[lane * LD + k] = sj;
+      }
+      if (lane == k) A[k * LD + k] = -inv;
+    }
+    __syncthreads();
+    PF_COUNT(26);
+  }
+  __syncthreads();
+}
+
+// u = A v for the symmetric swept matrix (lane p: u_p = sum_q A[q][p] v_q;
+// v staged in LDS, read by uniform broadcast)
+__device__ __forceinline__ double wave_symv(const double *A, int LD, int P, const double *v) {
+  const int p = pf_lane();
+  double u0 = 0.0, u1 = 0.0;
+  if (p < P) {
+    int q = 0;
+    for (; q + 1 < P; q += 2) {
+      u0 = fma(A[q * LD + p], v[q], u0);
+      u1 = fma(A[(q + 1) * LD + p], v[q + 1], u1);
+    }
+    if (q < P) u0 = fma(A[q * LD + p], v[q], u0);
+  }
+  return u0 + u1;
+}
+
 // Active-set solution of min gh.(z-x) + (z-x)'H(z-x)/2 + c||z_delta||_1 (wave 0).
-// Returns z in lane p; false if a factorisation failed.
+// Returns z in lane p; false if a pivot failed or the active set did not settle.
 template <int NW, int KMAX, int MODE>
 __device__ __forceinline__ bool qp_active(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, double x, double gh, double c,
                           double &z, int &nsolve) {
   const int lane = pf_lane();
   const int P = a.P, S = a.S, LD = sm.LD;
   const double *H = sm.U;
-  double *M = sm.U + (size_t)P * LD;
-  int *map = sm.qmap;
+  double *A = sm.U + (size_t)P * LD;
   const bool isd = (lane >= 2 && lane < 2 + S);
   bool zero = false;
   double sgn_ = 0.0;
@@ -251,43 +348,23 @@ __device__ __forceinline__ bool qp_active(const FitKArgs &a, FitSmem<NW, KMAX, M
     else if (x != 0.0 && sgx == -sgg) sgn_ = sgx;
     else sgn_ = -sgg;
   }
+  // A already holds H with every initially free coordinate swept in
+  // (sweep_in_free, all waves); a failed pivot there leaves flag[1] set
+  if (sm.flag[1]) return false;
   z = x;
   const int max_as = 2 * S + 16;
   for (int it = 0; it < max_as; ++it) {
     const bool fr = (lane < P) && !zero;
-    const unsigned long long fm = __ballot(fr);
-    const int n = __popcll(fm);
-    const int pos = __popcll(fm & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
-    if (fr) map[pos] = lane;
-    // dz for zero coords: (0 - x_q) ; x_q of zero coords enters the rhs
-    sm.pz[lane] = (lane < P && zero) ? x : 0.0;
+    // v: free -> gh + c s ; zero -> x  (so u_F = d_F, u_Z = gh_Z - model grad)
+    sm.pz[lane] = (lane < P) ? (zero ? x : gh + c * sgn_) : 0.0;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    double rhs = 0.0;
-    if (lane < n) {
-      const int pa = map[lane];
-      double v = 0.0;
-      for (int q = 0; q < P; ++q) v += H[pa * LD + q] * sm.pz[q];
-      rhs = v;
-      for (int b = 0; b < n; ++b) M[lane * LD + b] = H[pa * LD + map[b]];
-    }
-    // -(gh + c s) of the free coordinate at position `lane`
-    const double own = -(gh + c * sgn_);
-    sm.pd[lane] = own;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    if (lane < n) rhs += sm.pd[map[lane]];
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    if (!wave_chol_solve(M, LD, n, rhs)) return false;
+    PF_COUNT(27);
+    PF_STAMP(28);
+    const double u = wave_symv(A, LD, P, sm.pz);
+    PF_STAMP(29);
     ++nsolve;
-    // scatter the solution back to parameter lanes
-    sm.pd[lane] = rhs;  // position-indexed
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    const double zn = fr ? x + sm.pd[pos] : 0.0;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
+    const double zn = fr ? x + u : 0.0;
     // first sign crossing among free delta coordinates along z -> zn
     const bool viol = isd && fr && (zn * sgn_ < 0.0);
     const double tt = viol ? ((z != zn) ? z / (z - zn) : 0.0) : 2.0;
@@ -303,22 +380,15 @@ __device__ __forceinline__ bool qp_active(const FitKArgs &a, FitSmem<NW, KMAX, M
       const int jmin = __ffsll((long long)hit) - 1;
       z = (lane < P) ? z + tmin * (zn - z) : 0.0;
       if (lane == jmin) { z = 0.0; zero = true; sgn_ = 0.0; }
+      PF_STAMP(30);
+      if (!wave_sweep(A, LD, P, jmin, true)) return false;
+      PF_STAMP(31);
       continue;
     }
     z = (lane < P) ? zn : 0.0;
     // KKT of zero delta coordinates: |gh + H (z - x)| <= c
-    sm.pz[lane] = (lane < P) ? z - x : 0.0;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    double gq = 0.0;
     const bool cand = isd && zero;
-    if (cand) {
-      double v = gh;
-      for (int q = 0; q < P; ++q) v += H[lane * LD + q] * sm.pz[q];
-      gq = v;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
+    const double gq = cand ? gh - u : 0.0;
     const double sc = (cand && fabs(gq) > c * (1.0 + 1e-12)) ? fabs(gq) : -1.0;
     double smax = sc;
     smax = fmax(smax, shfl_xor_f64<1>(smax));
@@ -331,6 +401,7 @@ __device__ __forceinline__ bool qp_active(const FitKArgs &a, FitSmem<NW, KMAX, M
     const unsigned long long hit = __ballot(sc == smax && sc >= 0.0);
     const int jadd = __ffsll((long long)hit) - 1;
     if (lane == jadd) { zero = false; sgn_ = -((gq > 0.0) - (gq < 0.0)); }
+    if (!wave_sweep(A, LD, P, jadd, false)) return false;
   }
   return false;  // active set did not settle
 }
@@ -349,11 +420,17 @@ __device__ __forceinline__ bool polish_run(const FitKArgs &a, FitSmem<NW, KMAX, 
   bool cert = false;
   for (int it = 0; it < a.o.polish_max_iter; ++it) {
     const double gh = isd ? g - c * (double)((x > 0.0) - (x < 0.0)) : g;
+    PF_STAMP(20);
     hessian_collective<NW, KMAX, O0, O1, O2, MODE>(a, sm, x, gh, ws);
+    __syncthreads();
+    PF_STAMP(21);
+    sweep_in_free<NW, KMAX, MODE>(a, sm, gh, c);
+    PF_STAMP(24);
     if (wave == 0) {
       double z;
       int ns = 0;
       const bool ok = qp_active<NW, KMAX, MODE>(a, sm, x, gh, c, z, ns);
+      PF_STAMP(22);
       const double d = (lane < a.P) ? z - x : 0.0;
       double dec = wave_sum(gh * d);
       const double l1 = wave_sum(isd ? fabs(z) - fabs(x) : 0.0);
@@ -380,6 +457,7 @@ __device__ __forceinline__ bool polish_run(const FitKArgs &a, FitSmem<NW, KMAX, 
       if (!bad && fn <= f + 1e-4 * alpha * dec) { acc = true; break; }
       alpha *= 0.5;
     }
+    PF_STAMP(23);
     if (!acc) break;
     x = xn;
     f = fn;

@@ -36,3 +36,11 @@ for polish in (False,):
     print(f"   lbfgs_advance: state load {(v[7]-v[6])/ne:.0f}  step body {(v[8]-v[7])/ne:.0f} (per eval)")
     it = fit.n_iter[0].item()
     print(f"   LS_OK ({it} iters): fused-reduction {(v[11]-v[10])/it:.0f}  update+solve {(v[12]-v[11])/it:.0f} cycles/iter")
+# polish phases (block 0, all Newton iterations of all polish passes)
+torch.cuda.synchronize(); lib.pf_debug_stamps(buf, 1)
+t0 = time.time(); fit = eng.fit(grid, Yd); torch.cuda.synchronize(); dt = time.time() - t0
+lib.pf_debug_stamps(buf, 1)
+v = np.array(list(buf), dtype=np.float64)
+print(f"default fit {dt*1e3:.2f} ms; series0 n_eval={fit.n_eval[0].item()} status={fit.status[0].item()}")
+print(f"   polish: hessian {(v[21]-v[20]):.0f}  qp {(v[22]-v[21]):.0f}  line search {(v[23]-v[22]):.0f} cycles (total over Newton steps)")
+print(f"   qp: initial sweeps {v[26]:.0f} (to stamp24 {(v[24]-v[21]):.0f} cycles)  iterations {v[27]:.0f}  symv {(v[29]-v[28]):.0f}  rev-sweeps {(v[31]-v[30]):.0f} cycles")
