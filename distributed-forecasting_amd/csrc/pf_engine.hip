@@ -1198,7 +1198,7 @@ static_assert(sizeof(LbLds) + 16 <= kLbBytes, "LbLds too big");
 
 // ---------------------------------------------------------------- K3 kernel
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
-__global__ __launch_bounds__(NW * 64, 2) void k_fit(FitKArgs a) {
+__device__ __forceinline__ void fit_body(const FitKArgs &a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   FitSmem<NW, KMAX, MODE> sm;
   sm.carve(smem_raw, a.TQ, a.P);
@@ -1287,7 +1287,7 @@ __global__ __launch_bounds__(NW * 64, 2) void k_fit(FitKArgs a) {
 // budget (the L-BFGS kernel stays at 2 waves/SIMD).  Reads the Stan-phase
 // optimum from theta, re-evaluates f/g there, runs the proximal-Newton polish.
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
-__global__ __launch_bounds__(NW * 64, 2) void k_polish(FitKArgs a) {
+__device__ __forceinline__ void polish_body(const FitKArgs &a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   FitSmem<NW, KMAX, MODE> sm;
   sm.carve(smem_raw, a.TQ, a.P);
@@ -1302,16 +1302,34 @@ __global__ __launch_bounds__(NW * 64, 2) void k_polish(FitKArgs a) {
   double f, g;
   const bool bad = eval_collective<NW, KMAX, O0, O1, O2, MODE>(a, sm, x, f, g);
   if (bad) return;
-  int n_eval = 1, n_newton = 0;
+  int n_eval = 1, n_newton = 0;  // polish evaluations are not counted in n_eval[]
   const bool cert = polish_run<NW, KMAX, O0, O1, O2, MODE>(a, sm, x, f, g, n_eval, n_newton);
   if (threadIdx.x < 64) {
     if (lane < P) th_out[lane] = x;
     if (lane == 0) {
       a.f_out[s] = f;
-      a.n_eval[s] += n_eval;
       if (cert) a.status[s] = PF_ST_MAP;
     }
   }
+}
+
+// Entry points: the first pass and the resume passes are distinct kernels so
+// that traces and counters attribute them separately.
+template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
+__global__ __launch_bounds__(NW * 64, 2) void k_fit(FitKArgs a) {
+  fit_body<NW, KMAX, O0, O1, O2, MODE>(a);
+}
+template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
+__global__ __launch_bounds__(NW * 64, 2) void k_fit_resume(FitKArgs a) {
+  fit_body<NW, KMAX, O0, O1, O2, MODE>(a);
+}
+template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
+__global__ __launch_bounds__(NW * 64, 2) void k_polish(FitKArgs a) {
+  polish_body<NW, KMAX, O0, O1, O2, MODE>(a);
+}
+template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
+__global__ __launch_bounds__(NW * 64, 2) void k_polish_resume(FitKArgs a) {
+  polish_body<NW, KMAX, O0, O1, O2, MODE>(a);
 }
 
 // ============================================================================
@@ -1911,12 +1929,16 @@ int launch_fitlike(pf_ctx *ctx, bool fit, const FitKArgs &a, int n, hipStream_t 
   const size_t smem_p = FitSmem<NW, KMAX, MODE>::bytes(a.TQ, a.P, true);
   if (smem_p > 160 * 1024) return set_err(ctx, "fit: series too long for the LDS budget");
   if (fit) {
-    auto kern = k_fit<NW, KMAX, O0, O1, O2, MODE>;
-    auto kp = k_polish<NW, KMAX, O0, O1, O2, MODE>;
-    PF_HIP(ctx, hipFuncSetAttribute((const void *)kern,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
-    PF_HIP(ctx, hipFuncSetAttribute((const void *)kp,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem_p));
+    void (*kf[2])(FitKArgs) = {k_fit<NW, KMAX, O0, O1, O2, MODE>,
+                               k_fit_resume<NW, KMAX, O0, O1, O2, MODE>};
+    void (*kpl[2])(FitKArgs) = {k_polish<NW, KMAX, O0, O1, O2, MODE>,
+                                k_polish_resume<NW, KMAX, O0, O1, O2, MODE>};
+    for (int v = 0; v < 2; ++v) {
+      PF_HIP(ctx, hipFuncSetAttribute((const void *)kf[v],
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+      PF_HIP(ctx, hipFuncSetAttribute((const void *)kpl[v],
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem_p));
+    }
     const bool polish = a.o.polish && a.ws && a.growth == PF_GROWTH_LINEAR && a.K <= 32 && 2 + a.S <= 32;
     const int W = a.o.lbfgs_warmup;
     // passes: (cap, warm?) — warm-up, one more warm-up for uncertified
@@ -1935,11 +1957,12 @@ int launch_fitlike(pf_ctx *ctx, bool fit, const FitKArgs &a, int n, hipStream_t 
       b.o.max_iter = caps[ps];
       b.warm_cap = warm[ps];
       b.pass = ps;
-      PF_TIMED_LAUNCH(ctx, ps == 0 ? "k_fit" : "k_fit_resume", n, st, kern, dim3(n), dim3(NW * 64),
+      const int v = ps == 0 ? 0 : 1;
+      PF_TIMED_LAUNCH(ctx, v ? "k_fit_resume" : "k_fit", n, st, kf[v], dim3(n), dim3(NW * 64),
                       smem, st, b);
       PF_HIP(ctx, hipGetLastError());
       if (polish) {
-        PF_TIMED_LAUNCH(ctx, ps == 0 ? "k_polish" : "k_polish_resume", n, st, kp, dim3(n),
+        PF_TIMED_LAUNCH(ctx, v ? "k_polish_resume" : "k_polish", n, st, kpl[v], dim3(n),
                         dim3(NW * 64), smem_p, st, b);
         PF_HIP(ctx, hipGetLastError());
       }

@@ -159,8 +159,9 @@ int pf_objective_grad(pf_ctx *ctx, const pf_problem *pb, const double *theta,
  * f_stan[n] objective where the (first) L-BFGS phase stopped, status[n]
  * (in: PF_ST_CONSTANT rows are skipped; out: PF_ST_MAP when the polish
  * certified the optimum, else the Stan termination code), n_iter[n]
- * (L-BFGS iterations), n_eval[n] (objective+gradient evaluations, all
- * phases).  Scratch is stream-ordered in the context.                    */
+ * (L-BFGS iterations), n_eval[n] (L-BFGS objective+gradient evaluations,
+ * all passes; the polish's few line-search evaluations are not counted).
+ * Scratch is stream-ordered in the context.                              */
 int pf_fit(pf_ctx *ctx, const pf_problem *pb, const pf_fit_opts *opts,
            double *theta_inout, double *f_out, double *f_stan,
            int32_t *status, int32_t *n_iter, int32_t *n_eval, void *stream);
