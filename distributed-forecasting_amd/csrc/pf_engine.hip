@@ -213,8 +213,10 @@ __global__ void k_grid_segments(const double *__restrict__ t, int T, int Tp,
 // ============================================================================
 __global__ __launch_bounds__(256) void k_prepare(int T, int Tp, const double *__restrict__ t,
                                                  int growth, const double *__restrict__ y,
+                                                 const double *__restrict__ cap,
                                                  double *__restrict__ y_scale,
                                                  double *__restrict__ y_scaled,
+                                                 double *__restrict__ cap_scaled,
                                                  double *__restrict__ theta0,
                                                  int32_t *__restrict__ status, int P, int S) {
   __shared__ double red[3][4];
@@ -245,6 +247,12 @@ __global__ __launch_bounds__(256) void k_prepare(int T, int Tp, const double *__
     out[i] = v;
     if (i < T) vsum += v;
   }
+  if (growth == PF_GROWTH_LOGISTIC) {
+    // UPSTREAM initialize_scales: cap_scaled = (cap - floor) / y_scale, floor 0
+    const double *cs = cap + (size_t)s * Tp;
+    double *co = cap_scaled + (size_t)s * Tp;
+    for (int i = threadIdx.x; i < Tp; i += blockDim.x) co[i] = (i < T) ? cs[i] / scale : 0.0;
+  }
   vsum = wave_sum(vsum);
   __syncthreads();
   if (lane == 0) red[0][w] = vsum;
@@ -262,6 +270,19 @@ __global__ __launch_bounds__(256) void k_prepare(int T, int Tp, const double *__
     } else if (growth == PF_GROWTH_FLAT) {
       k = 0.0;
       m = vsum / (double)T;
+    } else {
+      // UPSTREAM logistic_growth_init
+      const double *cs = cap + (size_t)s * Tp;
+      const double Tt = t[T - 1] - t[0];
+      const double C0 = cs[0] / scale, C1 = cs[T - 1] / scale;
+      const double yy0 = fmax(0.01 * C0, fmin(0.99 * C0, y0));
+      const double yy1 = fmax(0.01 * C1, fmin(0.99 * C1, y1));
+      double r0 = C0 / yy0;
+      const double r1 = C1 / yy1;
+      if (fabs(r0 - r1) <= 0.01) r0 = 1.05 * r0;
+      const double L0 = log(r0 - 1.0), L1 = log(r1 - 1.0);
+      m = L0 * Tt / (L0 - L1);
+      k = (L0 - L1) / Tt;
     }
     th[0] = k;
     th[1] = m;
@@ -274,6 +295,9 @@ __global__ __launch_bounds__(256) void k_prepare(int T, int Tp, const double *__
 // K2/K3: objective + gradient (collective over one workgroup) and L-BFGS
 // ============================================================================
 enum { MODE_MULT = 0, MODE_ADD = 1, MODE_MIXED = 2 };
+// bit 2 of the MODE template argument selects the logistic-growth variant
+// (compiled separately so the linear kernels carry none of its registers)
+#define PF_MODE_LOGI 4
 
 struct FitKArgs {
   int T, Tp, K, S, growth, P, NB;
@@ -288,6 +312,7 @@ struct FitKArgs {
   const double *sigmas, *s_a, *s_m;
   double tau;
   const double *y_scaled;
+  const double *cap_scaled;  // [n][Tp] logistic capacity / y_scale (natural rows), else NULL
   double *ws;  // polish workspace [n][3][Tp]
   // fit
   double *theta;
@@ -407,7 +432,7 @@ struct LbLds;
 // reduction, H, Cholesky workspace} during the polish (k_polish).
 template <int NW, int KMAX, int MODE = 2>
 struct FitSmem {
-  static constexpr int NSET = (MODE == 2) ? 2 : 1;  // (mult, add) gradient sets
+  static constexpr int NSET = ((MODE & 3) == 2) ? 2 : 1;  // (mult, add) gradient sets
   static constexpr int NL = NW * 64;                 // row-pass threads
   double *y;        // [ny] lane-blocked y_scaled (position r*NL + L)
   double *th;       // [64]
@@ -482,6 +507,23 @@ struct FitSmem {
   }
 };
 
+// UPSTREAM logistic_gamma (prophet.stan): with k_s = k + sum_{j<s} delta_j in
+// lane s (s <= S) and t_change_s in lane s, returns the segment offsets
+// m_0 = m, m_{s+1} = m_s + (t_s - m_s)(1 - k_s/k_{s+1}) in lane s — Stan's
+// sequential order (one uniform FP64 chain; the ratios are lane-parallel).
+__device__ __forceinline__ double logistic_mseg(double kl, double tcl, double m, int S) {
+  const int lane = pf_lane();
+  const double kn = __shfl(kl, (lane + 1) & 63, 64);
+  const double rho = (lane < S) ? kl / kn : 0.0;
+  double mcur = m, ml = (lane == 0) ? m : 0.0;
+  for (int s = 0; s < S; ++s) {
+    const double tcs = readlane_f64(tcl, s), r = readlane_f64(rho, s);
+    mcur = mcur + (tcs - mcur) * (1.0 - r);
+    if (lane == s + 1) ml = mcur;
+  }
+  return ml;
+}
+
 template <int NW, int KMAX, int MODE>
 __device__ __forceinline__ void publish_theta(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, double x) {
   const int lane = pf_lane();
@@ -498,8 +540,15 @@ __device__ __forceinline__ void publish_theta(const FitKArgs &a, FitSmem<NW, KMA
   // kseg[s] = k + sum_{j<s} delta_j ; mseg[s] = m - sum_{j<s} tc_j delta_j
   const double cd_ex = wave_shift_up1(cd);
   const double ctd_ex = wave_shift_up1(ctd);
-  if (lane <= S) {
-    sm.kseg[lane] = k + (lane == 0 ? 0.0 : cd_ex);
+  const double kl = k + (lane == 0 ? 0.0 : cd_ex);
+  if constexpr ((MODE & PF_MODE_LOGI) != 0) {
+    const double ml = logistic_mseg(kl, sm.ctc[lane], m, S);
+    if (lane <= S) {
+      sm.kseg[lane] = kl;
+      sm.mseg[lane] = ml;
+    }
+  } else if (lane <= S) {
+    sm.kseg[lane] = kl;
     sm.mseg[lane] = m - (lane == 0 ? 0.0 : ctd_ex);
   }
   const double bval = __shfl(x, (lane + 3 + S) & 63, 64);
@@ -568,11 +617,13 @@ __device__ __forceinline__ void eval_rows(const FitKArgs &a, FitSmem<NW, KMAX, M
   double lbm[KMAX], lba[KMAX];
 #pragma unroll
   for (int f2 = 0; f2 < KMAX; ++f2) {
-    lbm[f2] = (MODE != MODE_ADD) ? sm.bm[f2] : 0.0;
-    lba[f2] = (MODE != MODE_MULT) ? sm.ba[f2] : 0.0;
+    lbm[f2] = ((MODE & 3) != MODE_ADD) ? sm.bm[f2] : 0.0;
+    lba[f2] = ((MODE & 3) != MODE_MULT) ? sm.ba[f2] : 0.0;
   }
   const double th_m = sm.th[1];
   const bool linear = (a.growth == PF_GROWTH_LINEAR);
+  constexpr bool logistic = (MODE & PF_MODE_LOGI) != 0;
+  const double *capr = logistic ? a.cap_scaled + (size_t)blockIdx.x * a.Tp : nullptr;
   double rr = 0.0, acc0 = 0.0, acc1 = 0.0;
   RowIn cur;
   if (R > 0) load_rowp<O0, O1, O2>(a, L, cur);
@@ -589,22 +640,39 @@ __device__ __forceinline__ void eval_rows(const FitKArgs &a, FitSmem<NW, KMAX, M
     double xm[4] = {0.0, 0.0, 0.0, 0.0}, xa[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int f2 = 0; f2 < KMAX; ++f2) {
-      if constexpr (MODE != MODE_ADD) xm[f2 & 3] = fma(xf[f2], lbm[f2], xm[f2 & 3]);
-      if constexpr (MODE != MODE_MULT) xa[f2 & 3] = fma(xf[f2], lba[f2], xa[f2 & 3]);
+      if constexpr ((MODE & 3) != MODE_ADD) xm[f2 & 3] = fma(xf[f2], lbm[f2], xm[f2 & 3]);
+      if constexpr ((MODE & 3) != MODE_MULT) xa[f2 & 3] = fma(xf[f2], lba[f2], xa[f2 & 3]);
     }
     const double xbm = (xm[0] + xm[1]) + (xm[2] + xm[3]);
     const double xba = (xa[0] + xa[1]) + (xa[2] + xa[3]);
-    const double tr = linear ? fma(sm.kseg[sg], ti, sm.mseg[sg]) : th_m;
+    // trend: linear k_s t + m_s; logistic cap sigma(k_s (t - m_s)); flat m
+    double tr, lgs = 0.0, capi = 0.0;
+    if constexpr (logistic) {
+      capi = valid ? capr[i] : 0.0;
+      lgs = 1.0 / (1.0 + exp(-(sm.kseg[sg] * (ti - sm.mseg[sg]))));
+      tr = capi * lgs;
+    } else {
+      tr = linear ? fma(sm.kseg[sg], ti, sm.mseg[sg]) : th_m;
+    }
     const double u = 1.0 + xbm;
     const double mu = fma(tr, u, xba);
     const double res = valid ? (sm.y[q] - mu) : 0.0;
     rr = fma(res, res, rr);
     const double G = res * u;
     const double cm = res * tr;
+    // per-row terms of the changepoint-block gradient, summed from each
+    // changepoint's first row (linear: G, G t; logistic, oracle PM/PK:
+    // -a k_s, a (t - m_s) with a = G cap sigma (1 - sigma))
+    double A0 = G, A1 = G * ti;
+    if constexpr (logistic) {
+      const double aa = G * capi * lgs * (1.0 - lgs);
+      A0 = -aa * sm.kseg[sg];
+      A1 = aa * (ti - sm.mseg[sg]);
+    }
 #pragma unroll
     for (int f2 = 0; f2 < KMAX; ++f2) {
-      if constexpr (MODE != MODE_ADD) gbm[f2] = fma(xf[f2], cm, gbm[f2]);
-      if constexpr (MODE != MODE_MULT) gba[f2] = fma(xf[f2], res, gba[f2]);
+      if constexpr ((MODE & 3) != MODE_ADD) gbm[f2] = fma(xf[f2], cm, gbm[f2]);
+      if constexpr ((MODE & 3) != MODE_MULT) gba[f2] = fma(xf[f2], res, gba[f2]);
     }
     // changepoints j in [sprev, sg) are first active at this row
     if (valid && sg > cur.sprev) {
@@ -614,8 +682,8 @@ __device__ __forceinline__ void eval_rows(const FitKArgs &a, FitSmem<NW, KMAX, M
         sm.cpl[j] = L;
       }
     }
-    acc0 += G;
-    acc1 = fma(G, ti, acc1);
+    acc0 += A0;
+    acc1 += A1;
     cur = nxt;
   }
   PF_STAMP(2);
@@ -632,12 +700,12 @@ __device__ __forceinline__ void eval_rows(const FitKArgs &a, FitSmem<NW, KMAX, M
     sm.rrw[wave] = rr;
   }
   // beta-gradient partials: transposed in-register reduction, one total per lane
-  constexpr int NS = (MODE == MODE_MIXED) ? 2 : 1;
+  constexpr int NS = ((MODE & 3) == MODE_MIXED) ? 2 : 1;
   double vv[NS * KMAX];
 #pragma unroll
   for (int f2 = 0; f2 < KMAX; ++f2) {
-    if constexpr (MODE == MODE_MULT) vv[f2] = gbm[f2];
-    else if constexpr (MODE == MODE_ADD) vv[f2] = gba[f2];
+    if constexpr ((MODE & 3) == MODE_MULT) vv[f2] = gbm[f2];
+    else if constexpr ((MODE & 3) == MODE_ADD) vv[f2] = gba[f2];
     else { vv[f2] = gbm[f2]; vv[KMAX + f2] = gba[f2]; }
   }
   transpose_store<NS * KMAX, 0>(vv, sm.gpart + (size_t)wave * NS * KMAX);
@@ -678,14 +746,68 @@ __device__ __forceinline__ bool eval_assemble(const FitKArgs &a, FitSmem<NW, KMA
   const double ls = x;  // meaningful in lane 2+S only
   double gv = 0.0, fterm = 0.0;
   const int p = lane;
+  // logistic: segment sums PM_s, PK_s (lane s) from the changepoint suffix
+  // sums, then reverse mode through logistic_gamma exactly in the oracle's
+  // order (orc_objective): uniform chains over s, lane-parallel otherwise.
+  constexpr bool logistic = (MODE & PF_MODE_LOGI) != 0;
+  double gkL = 0.0, gmL = 0.0, gdL = 0.0;
+  if constexpr (logistic) {
+    double su0 = 0.0, su1 = 0.0;
+    if (lane < S) {
+      const int Lj = sm.cpl[lane];
+      const int wj = Lj >> 6;
+      double l0 = 0.0, l1 = 0.0;
+#pragma unroll
+      for (int w2 = 0; w2 < NW; ++w2)
+        if (w2 > wj) { l0 += sm.wt0[w2]; l1 += sm.wt1[w2]; }
+      su0 = (sm.sfx0[Lj] + l0) - sm.cpre0[lane];
+      su1 = (sm.sfx1[Lj] + l1) - sm.cpre1[lane];
+    }
+    // segment s = [first row of cp s-1, first row of cp s)
+    const double pu0 = wave_shift_up1(su0), pu1 = wave_shift_up1(su1);
+    const double PMs = (lane == 0 ? tot0 : pu0) - (lane < S ? su0 : 0.0);
+    const double PKs = (lane == 0 ? tot1 : pu1) - (lane < S ? su1 : 0.0);
+    const double ks = (lane <= S) ? sm.kseg[lane] : 1.0;
+    const double kn = __shfl(ks, (lane + 1) & 63, 64);
+    const double ms = (lane <= S) ? sm.mseg[lane] : 0.0;
+    const double tcs = sm.ctc[lane];
+    const double rho = (lane < S) ? ks / kn : 0.0;
+    double PMt = readlane_f64(PMs, S), bar_l = 0.0;
+    for (int i = S - 1; i >= 0; --i) {
+      const double bar = PMt;
+      if (lane == i) bar_l = bar;
+      PMt = readlane_f64(PMs, i) + bar;
+      PMt += bar * (-(1.0 - readlane_f64(rho, i)));
+    }
+    gmL = PMt;
+    // PK[i] += bar_i (-(t_i - m_i)/k_{i+1});  PK[i+1] += bar_i (t_i - m_i) k_i / k_{i+1}^2
+    const double dtm = tcs - ms;
+    const double t1 = (lane < S) ? bar_l * (-dtm / kn) : 0.0;
+    const double t2 = (lane < S) ? bar_l * (dtm * ks / (kn * kn)) : 0.0;
+    const double PKf = (PKs + t1) + wave_shift_up1(t2);
+    // gd[s-1] = sum_{s' >= s} PK[s'] (s = S..1), gk = that + PK[0]
+    double sk = 0.0;
+    for (int s2 = S; s2 >= 1; --s2) {
+      sk += readlane_f64(PKf, s2);
+      if (lane == s2 + 1) gdL = sk;
+    }
+    gkL = sk + readlane_f64(PKf, 0);
+  }
   if (p == 0) {
     const double k = x;
-    gv = (linear ? -inv_s2 * tot1 : 0.0) + k / 25.0;
+    const double gk = logistic ? gkL : (linear ? tot1 : 0.0);
+    gv = -inv_s2 * gk + k / 25.0;
     fterm = k * k / 50.0;
   } else if (p == 1) {
     const double m = x;
-    gv = -inv_s2 * tot0 + m / 25.0;
+    const double gm = logistic ? gmL : tot0;
+    gv = -inv_s2 * gm + m / 25.0;
     fterm = m * m / 50.0;
+  } else if (p < 2 + S && logistic) {
+    const double d = x;
+    const double sg = (d > 0.0) - (d < 0.0);
+    gv = -inv_s2 * gdL + sg / a.tau;
+    fterm = fabs(d) / a.tau;
   } else if (p < 2 + S) {
     // suffix sums from changepoint j's first row: owner thread's inclusive
     // within-wave suffix + later waves - the owner's sum before that row
@@ -707,7 +829,7 @@ __device__ __forceinline__ bool eval_assemble(const FitKArgs &a, FitSmem<NW, KMA
     gv = (double)T - inv_s2 * rrt + 4.0 * sigma * sigma;
     fterm = 2.0 * sigma * sigma + (double)T * ls;
   } else if (p < P) {
-    constexpr int NS = (MODE == MODE_MIXED) ? 2 : 1;
+    constexpr int NS = ((MODE & 3) == MODE_MIXED) ? 2 : 1;
     const int f2 = p - 3 - S;
     const double bv = x;
     const double sgm = sm.csg[f2];
@@ -715,13 +837,13 @@ __device__ __forceinline__ bool eval_assemble(const FitKArgs &a, FitSmem<NW, KMA
 #pragma unroll
     for (int w2 = 0; w2 < NW; ++w2) {
       const double *gq = sm.gpart + (size_t)w2 * NS * KMAX;
-      if constexpr (MODE == MODE_MULT) gm += gq[f2];
-      else if constexpr (MODE == MODE_ADD) ga += gq[f2];
+      if constexpr ((MODE & 3) == MODE_MULT) gm += gq[f2];
+      else if constexpr ((MODE & 3) == MODE_ADD) ga += gq[f2];
       else { gm += gq[f2]; ga += gq[KMAX + f2]; }
     }
     double gl = 0.0;
-    if (MODE != MODE_ADD) gl += sm.csm[f2] * gm;
-    if (MODE != MODE_MULT) gl += sm.csa[f2] * ga;
+    if ((MODE & 3) != MODE_ADD) gl += sm.csm[f2] * gm;
+    if ((MODE & 3) != MODE_MULT) gl += sm.csa[f2] * ga;
     gv = -inv_s2 * gl + bv / (sgm * sgm);
     fterm = bv * bv / (2.0 * sgm * sgm);
   }
@@ -1353,6 +1475,7 @@ struct PredKArgs {
   float *comp;
   const uint32_t *series_id;  // RNG stream key per series (NULL: batch index)
   int method;                 // PF_INTERVAL_EXACT / PF_INTERVAL_SAMPLE
+  const double *cap;          // [n][Tp] logistic capacity / y_scale on the predicted rows
 };
 
 // k-th and (k+1)-th smallest of the wave's samples (v[q] = +inf if absent).
@@ -1434,8 +1557,15 @@ __device__ __forceinline__ void pred_setup(const PredKArgs &a, int series, PredS
   const double tcd = (lane < S) ? a.t_change[lane] * dval : 0.0;
   const double cd = wave_prefix_sum(dval), ctd = wave_prefix_sum(tcd);
   const double cd_ex = wave_shift_up1(cd), ctd_ex = wave_shift_up1(ctd);
-  if (lane <= S) {
-    ps.kseg[lane] = k + (lane == 0 ? 0.0 : cd_ex);
+  const double kl = k + (lane == 0 ? 0.0 : cd_ex);
+  if (a.growth == PF_GROWTH_LOGISTIC) {
+    const double ml = logistic_mseg(kl, (lane < S) ? a.t_change[lane] : 0.0, m, S);
+    if (lane <= S) {
+      ps.kseg[lane] = kl;
+      ps.mseg[lane] = ml;
+    }
+  } else if (lane <= S) {
+    ps.kseg[lane] = kl;
     ps.mseg[lane] = m - (lane == 0 ? 0.0 : ctd_ex);
   }
   const double bval = __shfl(x, (lane + 3 + S) & 63, 64);
@@ -1453,9 +1583,19 @@ __device__ __forceinline__ void pred_setup(const PredKArgs &a, int series, PredS
 
 // UPSTREAM sample_predictive_trend: T = t.max() of the frame being predicted
 // (rows sorted: the last valid row); the trend of a row is random iff
-// growth is linear, T > 1 and t > 1 (new changepoints live on (1, T]).
+// growth is linear or logistic, T > 1 and t > 1 (new changepoints live on
+// (1, T]).
 __device__ __forceinline__ bool pred_row_random(const PredKArgs &a, double ti, double t_max) {
-  return a.growth == PF_GROWTH_LINEAR && ti > 1.0 && t_max > 1.0;
+  return a.growth != PF_GROWTH_FLAT && ti > 1.0 && t_max > 1.0;
+}
+
+// point trend (scaled units) of a row on the fitted segments
+__device__ __forceinline__ double pred_trend(const PredKArgs &a, const PredSeries &ps, int series,
+                                             int row, double ti, int sg) {
+  if (a.growth == PF_GROWTH_LINEAR) return ps.kseg[sg] * ti + ps.mseg[sg];
+  if (a.growth == PF_GROWTH_LOGISTIC)
+    return a.cap[(size_t)series * a.Tp + row] / (1.0 + exp(-(ps.kseg[sg] * (ti - ps.mseg[sg]))));
+  return ps.mseg[0];
 }
 
 // ---- K4: point forecast + components + deterministic-row intervals.
@@ -1492,7 +1632,7 @@ __global__ __launch_bounds__(256) void k_predict_det(PredKArgs a) {
     for (int b = 0; b < 4; ++b)
       if (b < a.n_comp) a.comp[((size_t)b * a.n_series + series) * a.Tp + row] = (float)cb[b];
   }
-  const double trs = (a.growth == PF_GROWTH_LINEAR) ? (ps.kseg[sg] * ti + ps.mseg[sg]) : ps.mseg[0];
+  const double trs = pred_trend(a, ps, series, row, ti, sg);
   const double trend = trs * ysc;
   const double addt = xba * ysc;
   const double yhat = trend * (1.0 + xbm) + addt;
@@ -1534,6 +1674,7 @@ __global__ __launch_bounds__(256) void k_predict_det(PredKArgs a) {
 // counter-based stream (same draws, evaluated in fp64).
 #define PF_MC_NCP 6
 #define PF_MC_WAVES_PER_SERIES 16
+#define PF_MC_WPB 8  // waves per block (VGPR budget: 2 waves/SIMD)
 
 __device__ __forceinline__ void mc_sample_cp(uint32_t seed0, uint32_t seed1, uint32_t series, int smp,
                                              int c, double t_max, double lam, double &tc, double &dl) {
@@ -1574,12 +1715,37 @@ __device__ __noinline__ double mc_offset_slow(uint32_t seed0, uint32_t seed1, ui
   return off;
 }
 
-template <int KMAX>
-__global__ __launch_bounds__(256) void k_predict_mc(PredKArgs a) {
+// logistic trend sample (scaled units, without cap) at ti: walk the
+// sample's new changepoints in time order from the last fitted segment
+// (UPSTREAM piecewise_logistic over the concatenated changepoints)
+__device__ __noinline__ double mc_logistic_slow(uint32_t seed0, uint32_t seed1, uint32_t series, int smp,
+                                                int n, double t_max, double lam, double ti, double k0,
+                                                double m0) {
+  double tcs[32], dls[32];
+  const int nn = n < 32 ? n : 32;
+  for (int c = 0; c < nn; ++c) {
+    double tc, dl;
+    mc_sample_cp(seed0, seed1, series, smp, c, t_max, lam, tc, dl);
+    int q = c;
+    while (q > 0 && tcs[q - 1] > tc) { tcs[q] = tcs[q - 1]; dls[q] = dls[q - 1]; --q; }
+    tcs[q] = tc;
+    dls[q] = dl;
+  }
+  double kc = k0, mc = m0;
+  for (int c = 0; c < nn && ti >= tcs[c]; ++c) {
+    const double kn = kc + dls[c];
+    mc = mc + (tcs[c] - mc) * (1.0 - kc / kn);
+    kc = kn;
+  }
+  return 1.0 / (1.0 + exp(-(kc * (ti - mc))));
+}
+
+template <int KMAX, int WPB>
+__global__ __launch_bounds__(WPB * 64) void k_predict_mc(PredKArgs a) {
   __shared__ PredSeries ps;
   __shared__ float2 s_cp[PF_MC_NCP][64 * PF_NQ];   // (t_c, delta) per sample
   __shared__ int s_cnt[64 * PF_NQ];
-  __shared__ float s_buf[4][64];
+  __shared__ float s_buf[WPB][64];
   __shared__ int s_r0;
   const int series = blockIdx.y, lane = pf_lane(), wave = pf_wave();
   const uint32_t sid = a.series_id ? a.series_id[series] : (uint32_t)series;
@@ -1606,19 +1772,22 @@ __global__ __launch_bounds__(256) void k_predict_mc(PredKArgs a) {
   const double lam_pois = any_random ? (double)a.S * (t_max - 1.0) : 0.0;
   if (any_random) {
     const double e_neg = exp(-lam_pois);
-    for (int smp = threadIdx.x; smp < a.N; smp += 256) {
+    for (int smp = threadIdx.x; smp < a.N; smp += WPB * 64) {
       const int n = mc_sample_count(a.seed0, a.seed1, sid, smp, lam_pois, e_neg);
       s_cnt[smp] = n;
       for (int c = 0; c < n && c < PF_MC_NCP; ++c) {
         double tc, dl;
         mc_sample_cp(a.seed0, a.seed1, sid, smp, c, t_max, lam, tc, dl);
-        s_cp[c][smp] = make_float2((float)tc, (float)dl);
+        // kept in time order (logistic walks them in order; linear sums)
+        int q = c;
+        while (q > 0 && s_cp[q - 1][smp].x > (float)tc) { s_cp[q][smp] = s_cp[q - 1][smp]; --q; }
+        s_cp[q][smp] = make_float2((float)tc, (float)dl);
       }
     }
   }
   __syncthreads();
-  const int stride = gridDim.x * 4;
-  for (int row = r0 + blockIdx.x * 4 + wave; row < a.Tf; row += stride) {
+  const int stride = gridDim.x * WPB;
+  for (int row = r0 + blockIdx.x * WPB + wave; row < a.Tf; row += stride) {
     const double ti = a.t[row];
     const int sg = a.seg[row];
     double xbm = 0.0, xba = 0.0;
@@ -1629,11 +1798,13 @@ __global__ __launch_bounds__(256) void k_predict_mc(PredKArgs a) {
     }
     xbm = wave_sum(xbm);
     xba = wave_sum(xba);
-    const double trs = (a.growth == PF_GROWTH_LINEAR) ? (ps.kseg[sg] * ti + ps.mseg[sg]) : ps.mseg[0];
+    const double trs = pred_trend(a, ps, series, row, ti, sg);
     const double trend = trs * ysc;
     const double addt = xba * ysc;
     const double yhat = trend * (1.0 + xbm) + addt;
     float ylo, yhi, tlo = (float)trend, thi = (float)trend;
+    const bool logi = a.growth == PF_GROWTH_LOGISTIC;
+    const double capr = logi ? a.cap[(size_t)series * a.Tp + row] : 0.0;
     float z[PF_NQ];
 #pragma unroll
     for (int c = 0; c < PF_NQ / 4; ++c) {
@@ -1661,16 +1832,34 @@ __global__ __launch_bounds__(256) void k_predict_mc(PredKArgs a) {
         const int smp = lane + 64 * q;
         if (smp < a.N) {
           const int n = s_cnt[smp];
-          float off = 0.0f;
-          if (n <= PF_MC_NCP) {
+          float trs_s;
+          if (!logi) {
+            float off = 0.0f;
+            if (n <= PF_MC_NCP) {
+              for (int c = 0; c < n; ++c) {
+                const float2 cp = s_cp[c][smp];
+                off = (tf >= cp.x) ? fmaf(cp.y, tf - cp.x, off) : off;
+              }
+            } else {
+              off = (float)mc_offset_slow(a.seed0, a.seed1, sid, smp, n, t_max, lam, ti);
+            }
+            trs_s = (float)trend + ysf * off;
+          } else if (n <= PF_MC_NCP && (n == 0 || tf < s_cp[0][smp].x)) {
+            trs_s = (float)trend;  // no new changepoint before t
+          } else if (n <= PF_MC_NCP) {
+            float kc = (float)ps.kseg[a.S], mc = (float)ps.mseg[a.S];
             for (int c = 0; c < n; ++c) {
               const float2 cp = s_cp[c][smp];
-              off = (tf >= cp.x) ? fmaf(cp.y, tf - cp.x, off) : off;
+              if (tf < cp.x) break;
+              const float kn = kc + cp.y;
+              mc = mc + (cp.x - mc) * (1.0f - kc / kn);
+              kc = kn;
             }
+            trs_s = (float)(ysc * capr) / (1.0f + __expf(-(kc * (tf - mc))));
           } else {
-            off = (float)mc_offset_slow(a.seed0, a.seed1, sid, smp, n, t_max, lam, ti);
+            trs_s = (float)(ysc * capr * mc_logistic_slow(a.seed0, a.seed1, sid, smp, n, t_max, lam, ti,
+                                                          ps.kseg[a.S], ps.mseg[a.S]));
           }
-          const float trs_s = (float)trend + ysf * off;
           tv[q] = trs_s;
           v[q] = fmaf(sd, z[q], fmaf(trs_s, u1, addf));
         } else {
@@ -1854,16 +2043,15 @@ int pf_build_grid(pf_ctx *ctx, const int64_t *ds_ns, int T, int T_pad, int64_t s
 int pf_prepare(pf_ctx *ctx, int n_series, const pf_grid *grid, int growth, const double *y,
                const double *cap, double *y_scale, double *y_scaled, double *cap_scaled,
                double *theta0, int32_t *status, void *stream) {
-  (void)cap;
-  (void)cap_scaled;
-  if (growth == PF_GROWTH_LOGISTIC) return set_err(ctx, "pf_prepare: logistic growth not supported on the GPU path yet");
   if (n_series < 0 || !grid || !y || !y_scale || !y_scaled || !theta0 || !status)
     return set_err(ctx, "pf_prepare: bad arguments");
+  if (growth == PF_GROWTH_LOGISTIC && (!cap || !cap_scaled))
+    return set_err(ctx, "pf_prepare: logistic growth needs cap and cap_scaled");
   if (n_series == 0) return 0;
   const int P = 3 + grid->S + grid->K;
   PF_TIMED_LAUNCH(ctx, "k_prepare", n_series, (hipStream_t)stream, k_prepare, dim3(n_series),
                   dim3(256), 0, (hipStream_t)stream, grid->T, grid->T_pad, grid->t, growth, y,
-                  y_scale, y_scaled, theta0, status, P, grid->S);
+                  cap, y_scale, y_scaled, cap_scaled, theta0, status, P, grid->S);
   PF_HIP(ctx, hipGetLastError());
   return 0;
 }
@@ -1920,26 +2108,36 @@ FitKArgs make_fit_args(const pf_problem *pb) {
   a.s_m = pb->s_m;
   a.tau = pb->tau;
   a.y_scaled = pb->y_scaled;
+  a.cap_scaled = pb->cap_scaled;
   return a;
 }
 
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
 int launch_fitlike(pf_ctx *ctx, bool fit, const FitKArgs &a, int n, hipStream_t st) {
+  // the polish handles K <= 32 and 2 + S <= 32 (J space of two 32-column blocks)
+  constexpr bool HAS_POLISH = KMAX <= 32 && (MODE & PF_MODE_LOGI) == 0;
   const size_t smem = FitSmem<NW, KMAX, MODE>::bytes(a.TQ, a.P, false);
-  const size_t smem_p = FitSmem<NW, KMAX, MODE>::bytes(a.TQ, a.P, true);
-  if (smem_p > 160 * 1024) return set_err(ctx, "fit: series too long for the LDS budget");
+  const size_t smem_p = FitSmem<NW, KMAX, MODE>::bytes(a.TQ, a.P, HAS_POLISH);
+  if (smem > 160 * 1024) return set_err(ctx, "fit: series too long for the LDS budget");
   if (fit) {
     void (*kf[2])(FitKArgs) = {k_fit<NW, KMAX, O0, O1, O2, MODE>,
                                k_fit_resume<NW, KMAX, O0, O1, O2, MODE>};
-    void (*kpl[2])(FitKArgs) = {k_polish<NW, KMAX, O0, O1, O2, MODE>,
-                                k_polish_resume<NW, KMAX, O0, O1, O2, MODE>};
-    for (int v = 0; v < 2; ++v) {
+    for (int v = 0; v < 2; ++v)
       PF_HIP(ctx, hipFuncSetAttribute((const void *)kf[v],
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
-      PF_HIP(ctx, hipFuncSetAttribute((const void *)kpl[v],
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem_p));
+    bool polish = a.o.polish && a.ws && a.growth == PF_GROWTH_LINEAR && a.K <= 32 && 2 + a.S <= 32 &&
+                  smem_p <= 160 * 1024;
+    void (*kpl[2])(FitKArgs) = {nullptr, nullptr};
+    if constexpr (HAS_POLISH) {
+      kpl[0] = k_polish<NW, KMAX, O0, O1, O2, MODE>;
+      kpl[1] = k_polish_resume<NW, KMAX, O0, O1, O2, MODE>;
+      if (polish)
+        for (int v = 0; v < 2; ++v)
+          PF_HIP(ctx, hipFuncSetAttribute((const void *)kpl[v],
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem_p));
+    } else {
+      polish = false;
     }
-    const bool polish = a.o.polish && a.ws && a.growth == PF_GROWTH_LINEAR && a.K <= 32 && 2 + a.S <= 32;
     const int W = a.o.lbfgs_warmup;
     // passes: (cap, warm?) — warm-up, one more warm-up for uncertified
     // series, then Stan's full rules; each followed by the polish
@@ -1981,14 +2179,28 @@ int launch_fitlike(pf_ctx *ctx, bool fit, const FitKArgs &a, int n, hipStream_t 
 //   (26, 10,3,0, MULT) — the reference's configuration (yearly 10 + weekly 3,
 //                        multiplicative): features regenerated in-register
 //   (26, 10,3,0, ADD/MIXED) — same grid, other seasonality modes
-//   dense fallbacks KMAX 32 / 64 (any K <= KMAX), features read from X^T.
-int dispatch_fitlike(pf_ctx *ctx, bool fit, const FitKArgs &a, int n, int fourier103, int mode,
+//   (34, 10,3,4, MULT) — sub-daily data (yearly + weekly + daily 4; config 5)
+//   dense fallbacks KMAX 32 / 61 (any K <= KMAX), features read from X^T.
+int dispatch_fitlike(pf_ctx *ctx, bool fit, const FitKArgs &a, int n, const int32_t *orders, int mode,
                      hipStream_t st) {
-  if (fourier103 && a.K == 26) {
+  const bool o1030 = orders[0] == 10 && orders[1] == 3 && orders[2] == 0;
+  const bool o1034 = orders[0] == 10 && orders[1] == 3 && orders[2] == 4;
+  constexpr int LG = PF_MODE_LOGI;
+  if (a.growth == PF_GROWTH_LOGISTIC) {
+    if (o1030 && a.K == 26 && mode == MODE_MULT)
+      return launch_fitlike<PF_FIT_NW, 26, 10, 3, 0, MODE_MULT | LG>(ctx, fit, a, n, st);
+    if (o1034 && a.K == 34 && mode == MODE_MULT)
+      return launch_fitlike<PF_FIT_NW, 34, 10, 3, 4, MODE_MULT | LG>(ctx, fit, a, n, st);
+    if (a.K <= 32) return launch_fitlike<PF_FIT_NW, 32, 0, 0, 0, MODE_MIXED | LG>(ctx, fit, a, n, st);
+    return set_err(ctx, "fit: logistic growth supports K <= 32, or yearly+weekly+daily (K = 34) multiplicative");
+  }
+  if (o1030 && a.K == 26) {
     if (mode == MODE_MULT) return launch_fitlike<PF_FIT_NW, 26, 10, 3, 0, MODE_MULT>(ctx, fit, a, n, st);
     if (mode == MODE_ADD) return launch_fitlike<PF_FIT_NW, 26, 10, 3, 0, MODE_ADD>(ctx, fit, a, n, st);
     return launch_fitlike<PF_FIT_NW, 26, 10, 3, 0, MODE_MIXED>(ctx, fit, a, n, st);
   }
+  if (o1034 && a.K == 34 && mode == MODE_MULT)
+    return launch_fitlike<PF_FIT_NW, 34, 10, 3, 4, MODE_MULT>(ctx, fit, a, n, st);
   if (a.K <= 32) return launch_fitlike<PF_FIT_NW, 32, 0, 0, 0, MODE_MIXED>(ctx, fit, a, n, st);
   if (a.K <= 61) return launch_fitlike<PF_FIT_NW, 61, 0, 0, 0, MODE_MIXED>(ctx, fit, a, n, st);
   return set_err(ctx, "fit: K > 61 not supported");
@@ -2022,16 +2234,14 @@ static int prepare_fit_scratch(pf_ctx *ctx, FitKArgs &a, int n_series, bool poli
   return 0;
 }
 
-static int is_fourier103(const pf_problem *pb) {
-  return pb->fourier_orders[0] == 10 && pb->fourier_orders[1] == 3 && pb->fourier_orders[2] == 0;
-}
 static int mode_of(const pf_problem *pb) {
   return (pb->season_mode == 0) ? MODE_MULT : (pb->season_mode == 1) ? MODE_ADD : MODE_MIXED;
 }
 
 static int check_problem(pf_ctx *ctx, const pf_problem *pb) {
   if (!pb) return set_err(ctx, "NULL problem");
-  if (pb->growth == PF_GROWTH_LOGISTIC) return set_err(ctx, "logistic growth not supported on the GPU path yet");
+  if (pb->growth == PF_GROWTH_LOGISTIC && !pb->cap_scaled)
+    return set_err(ctx, "logistic growth needs cap_scaled");
   const int P = 3 + pb->grid.S + pb->grid.K;
   if (P > 64) return set_err(ctx, "P = 3 + S + K must be <= 64 on this build");
   if (pb->grid.S < 1 || pb->grid.S > 62) return set_err(ctx, "S out of range");
@@ -2053,7 +2263,7 @@ int pf_objective_grad(pf_ctx *ctx, const pf_problem *pb, const double *theta, do
   a.g_out = g;
   rc = prepare_fit_scratch(ctx, a, pb->n_series, false, (hipStream_t)stream);
   if (rc) return rc;
-  return dispatch_fitlike(ctx, false, a, pb->n_series, is_fourier103(pb), mode_of(pb),
+  return dispatch_fitlike(ctx, false, a, pb->n_series, pb->fourier_orders, mode_of(pb),
                           (hipStream_t)stream);
 }
 
@@ -2075,13 +2285,12 @@ int pf_fit(pf_ctx *ctx, const pf_problem *pb, const pf_fit_opts *opts, double *t
   a.o = *opts;
   rc = prepare_fit_scratch(ctx, a, pb->n_series, opts->polish != 0, (hipStream_t)stream);
   if (rc) return rc;
-  return dispatch_fitlike(ctx, true, a, pb->n_series, is_fourier103(pb), mode_of(pb),
+  return dispatch_fitlike(ctx, true, a, pb->n_series, pb->fourier_orders, mode_of(pb),
                           (hipStream_t)stream);
 }
 
 int pf_predict(pf_ctx *ctx, const pf_predict_args *p, void *stream) {
   if (!p) return set_err(ctx, "pf_predict: NULL args");
-  if (p->growth == PF_GROWTH_LOGISTIC) return set_err(ctx, "pf_predict: logistic growth not supported on the GPU path yet");
   if (p->n_samples < 0 || p->n_samples > 64 * PF_NQ) return set_err(ctx, "pf_predict: n_samples must be in [0, 1024]");
   const int P = 3 + p->fg.S + p->fg.K;
   if (P > 64 || p->fg.K > 64) return set_err(ctx, "pf_predict: P must be <= 64");
@@ -2147,6 +2356,9 @@ int pf_predict(pf_ctx *ctx, const pf_predict_args *p, void *stream) {
     if (a.N == 1) { a.k_lo = 0; a.fr_lo = 0.f; a.k_hi_neg = 0; a.fr_hi = 0.f; }
   }
   a.method = p->interval_method;
+  a.cap = p->cap_scaled;
+  if (a.growth == PF_GROWTH_LOGISTIC && !a.cap)
+    return set_err(ctx, "pf_predict: logistic growth needs cap_scaled on the predicted rows");
   if (a.method != PF_INTERVAL_EXACT && a.method != PF_INTERVAL_SAMPLE)
     return set_err(ctx, "pf_predict: interval_method must be PF_INTERVAL_EXACT or PF_INTERVAL_SAMPLE");
   const dim3 grid((a.Tf + 255) / 256, a.n_series);
@@ -2156,12 +2368,14 @@ int pf_predict(pf_ctx *ctx, const pf_predict_args *p, void *stream) {
   if (a.N > 0) {
     // sample mode: ~8 rows per wave; exact mode: the random rows (the
     // horizon) spread over PF_MC_WAVES_PER_SERIES waves per series
-    int gx = (a.method == PF_INTERVAL_SAMPLE) ? (a.Tf + 31) / 32 : PF_MC_WAVES_PER_SERIES / 4;
-    if (gx > (a.Tf + 3) / 4) gx = (a.Tf + 3) / 4;
+    int gx = (a.method == PF_INTERVAL_SAMPLE) ? (a.Tf + 8 * PF_MC_WPB - 1) / (8 * PF_MC_WPB)
+                                              : PF_MC_WAVES_PER_SERIES / PF_MC_WPB;
+    if (gx > (a.Tf + PF_MC_WPB - 1) / PF_MC_WPB) gx = (a.Tf + PF_MC_WPB - 1) / PF_MC_WPB;
     if (gx < 1) gx = 1;
     const dim3 gmc(gx, a.n_series);
     PF_TIMED_LAUNCH(ctx, "k_predict_mc", gmc.x * gmc.y, (hipStream_t)stream,
-                    (k_predict_mc<64>), gmc, dim3(256), 0, (hipStream_t)stream, a);
+                    (k_predict_mc<64, PF_MC_WPB>), gmc, dim3(PF_MC_WPB * 64), 0,
+                    (hipStream_t)stream, a);
     PF_HIP(ctx, hipGetLastError());
   }
   return 0;

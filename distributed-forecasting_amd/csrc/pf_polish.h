@@ -61,8 +61,8 @@ __device__ __forceinline__ void hessian_collective(const FitKArgs &a, FitSmem<NW
     double xm[4] = {0.0, 0.0, 0.0, 0.0}, xa[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int f2 = 0; f2 < KMAX; ++f2) {
-      if constexpr (MODE != MODE_ADD) xm[f2 & 3] = fma(xf[f2], sm.bm[f2], xm[f2 & 3]);
-      if constexpr (MODE != MODE_MULT) xa[f2 & 3] = fma(xf[f2], sm.ba[f2], xa[f2 & 3]);
+      if constexpr ((MODE & 3) != MODE_ADD) xm[f2 & 3] = fma(xf[f2], sm.bm[f2], xm[f2 & 3]);
+      if constexpr ((MODE & 3) != MODE_MULT) xa[f2 & 3] = fma(xf[f2], sm.ba[f2], xa[f2 & 3]);
       if ((f2 & 7) == 7) __builtin_amdgcn_sched_barrier(0);
     }
     const double xbm = (xm[0] + xm[1]) + (xm[2] + xm[3]);

@@ -260,7 +260,8 @@ class Engine:
             self._vec_cache[key] = (sig, s_a, s_m, 0 if mult else 1)
         return self._vec_cache[key]
 
-    def problem(self, grid: DeviceGrid, y_scaled: torch.Tensor, n: int) -> L.PfProblem:
+    def problem(self, grid: DeviceGrid, y_scaled: torch.Tensor, n: int,
+                cap_scaled: torch.Tensor | None = None) -> L.PfProblem:
         sig, s_a, s_m, mode = self._vectors(grid)
         pb = L.PfProblem()
         pb.n_series = n
@@ -269,16 +270,23 @@ class Engine:
         pb.grid = grid.as_pf()
         pb.sigmas, pb.s_a, pb.s_m = sig.data_ptr(), s_a.data_ptr(), s_m.data_ptr()
         pb.y_scaled = y_scaled.data_ptr()
-        pb.cap_scaled = None
+        if self.config.growth == "logistic":
+            if cap_scaled is None:
+                raise ValueError("logistic growth needs cap_scaled")
+            pb.cap_scaled = cap_scaled.data_ptr()
+        else:
+            pb.cap_scaled = None
         fo = grid.fourier_orders
         for i in range(3):
             pb.fourier_orders[i] = fo[i]
         pb.season_mode = mode
-        pb._keep = (sig, s_a, s_m, y_scaled)
+        pb._keep = (sig, s_a, s_m, y_scaled, cap_scaled)
         return pb
 
-    def prepare(self, grid: DeviceGrid, Y: torch.Tensor):
-        """y_scale, y_scaled and Prophet's init theta0 on the device."""
+    def prepare(self, grid: DeviceGrid, Y: torch.Tensor, cap: torch.Tensor | None = None):
+        """y_scale, y_scaled, Prophet's init theta0, status and (logistic
+        growth) cap_scaled on the device.  ``cap`` [n, T_pad] float64 is the
+        capacity column (UPSTREAM 'cap'), required for logistic growth."""
         n = Y.shape[0]
         assert Y.dtype == torch.float64 and Y.shape[1] == grid.T_pad and Y.is_contiguous()
         dev = Y.device
@@ -287,19 +295,28 @@ class Engine:
         y_scaled = torch.empty_like(Y)
         theta = torch.empty((n, P), dtype=torch.float64, device=dev)
         status = torch.empty(n, dtype=torch.int32, device=dev)
+        cap_scaled = None
+        if self.config.growth == "logistic":
+            if cap is None:
+                raise ValueError('Capacities must be supplied for logistic growth in column "cap"')
+            assert cap.dtype == torch.float64 and cap.shape == Y.shape and cap.is_contiguous()
+            cap_scaled = torch.empty_like(Y)
         pg = grid.as_pf()
         rc = self.ctx.lib.pf_prepare(self.ctx.h, n, ctypes.byref(pg),
-                                     L.PF_GROWTH[self.config.growth], _ptr(Y), None,
-                                     _ptr(y_scale), _ptr(y_scaled), None, _ptr(theta),
-                                     _ptr(status), _stream(self.device))
+                                     L.PF_GROWTH[self.config.growth], _ptr(Y),
+                                     _ptr(cap) if cap_scaled is not None else None,
+                                     _ptr(y_scale), _ptr(y_scaled),
+                                     _ptr(cap_scaled) if cap_scaled is not None else None,
+                                     _ptr(theta), _ptr(status), _stream(self.device))
         self.ctx.check(rc, "pf_prepare")
-        return y_scale, y_scaled, theta, status
+        return y_scale, y_scaled, theta, status, cap_scaled
 
-    def objective_grad(self, grid: DeviceGrid, y_scaled: torch.Tensor, theta: torch.Tensor):
+    def objective_grad(self, grid: DeviceGrid, y_scaled: torch.Tensor, theta: torch.Tensor,
+                       cap_scaled: torch.Tensor | None = None):
         n = theta.shape[0]
         f = torch.empty(n, dtype=torch.float64, device=theta.device)
         g = torch.empty_like(theta)
-        pb = self.problem(grid, y_scaled, n)
+        pb = self.problem(grid, y_scaled, n, cap_scaled)
         rc = self.ctx.lib.pf_objective_grad(self.ctx.h, ctypes.byref(pb), _ptr(theta), _ptr(f),
                                             _ptr(g), _stream(self.device))
         self.ctx.check(rc, "pf_objective_grad")
@@ -319,7 +336,7 @@ class Engine:
         return o
 
     def fit(self, grid: DeviceGrid, Y: torch.Tensor, polish: bool = True,
-            stan_faithful: bool = False, **opt) -> FitResult:
+            stan_faithful: bool = False, cap: torch.Tensor | None = None, **opt) -> FitResult:
         """Fit every row of Y [n, T_pad] (raw y, float64, on this GPU).
 
         Default: Stan L-BFGS warm-up (<= lbfgs_warmup iterations) handed to
@@ -328,13 +345,13 @@ class Engine:
         termination rules (the reference's optimizer run), then polishes to
         the same MAP; ``polish=False`` stops where Stan stops."""
         n = Y.shape[0]
-        y_scale, y_scaled, theta, status = self.prepare(grid, Y)
+        y_scale, y_scaled, theta, status, cap_scaled = self.prepare(grid, Y, cap)
         dev = Y.device
         f = torch.empty(n, dtype=torch.float64, device=dev)
         f_stan = torch.empty(n, dtype=torch.float64, device=dev)
         n_iter = torch.empty(n, dtype=torch.int32, device=dev)
         n_eval = torch.empty(n, dtype=torch.int32, device=dev)
-        pb = self.problem(grid, y_scaled, n)
+        pb = self.problem(grid, y_scaled, n, cap_scaled)
         o = self.fit_opts(polish, stan_faithful, **opt)
         rc = self.ctx.lib.pf_fit(self.ctx.h, ctypes.byref(pb), ctypes.byref(o), _ptr(theta),
                                  _ptr(f), _ptr(f_stan), _ptr(status), _ptr(n_iter), _ptr(n_eval),
@@ -351,7 +368,8 @@ class Engine:
     def predict(self, fit: FitResult, fgrid: DeviceGrid, n_samples: int | None = None,
                 seed: int = 0, components: bool = True,
                 series_id: torch.Tensor | None = None,
-                interval_method: str | None = None) -> dict:
+                interval_method: str | None = None,
+                cap: torch.Tensor | None = None) -> dict:
         """Point forecast + MC intervals for every fitted series on ``fgrid``.
         Returns float32 device tensors [n, fgrid.T_pad] (valid columns :T).
         ``series_id`` (int32/uint32 [n] on the device) keys each series' RNG
@@ -378,7 +396,15 @@ class Engine:
         a.s_a, a.s_m = s_a.data_ptr(), s_m.data_ptr()
         a.theta = fit.theta.data_ptr()
         a.y_scale = fit.y_scale.data_ptr()
-        a.cap_scaled = None
+        cap_s = None
+        if self.config.growth == "logistic":
+            if cap is None:
+                raise ValueError('Capacities must be supplied for logistic growth in column "cap"')
+            assert cap.shape == (n, fgrid.T_pad)
+            cap_s = (cap.to(torch.float64) / fit.y_scale[:, None]).contiguous()
+            a.cap_scaled = cap_s.data_ptr()
+        else:
+            a.cap_scaled = None
         a.interval_width = float(self.config.interval_width)
         a.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         a.yhat, a.yhat_lower, a.yhat_upper = (out[k].data_ptr() for k in

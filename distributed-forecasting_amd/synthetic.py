@@ -56,3 +56,37 @@ def store_item_frame(n_stores: int = 10, n_items: int = 50, start="2013-01-01",
         "item": np.repeat(items, T).astype(np.int32),
         "y": Y.reshape(-1),
     })
+
+
+NS_PER_HOUR = 3_600_000_000_000
+
+
+def hourly_dates(start="2017-01-01", n_hours: int = 8760) -> np.ndarray:
+    """SURVEY.md §8d config 5 grid: ``start`` 00:00 + k hours."""
+    s = np.datetime64(start, "D").astype("datetime64[ns]").astype(np.int64)
+    return s + NS_PER_HOUR * np.arange(n_hours, dtype=np.int64)
+
+
+def saturating_matrix(n_series: int, ds_ns: np.ndarray, seed: int = 20261015 + 4):
+    """Config-5-shaped series for logistic growth: a saturating level
+    C_s sigma(r_s (t - t0_s)) with yearly, weekly and (for sub-daily grids)
+    daily multiplicative seasonality and noise.  Returns (Y, cap) with the
+    constant capacity cap_s = 1.2 max(y_s)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    T = ds_ns.shape[0]
+    d = (ds_ns / 1e9) / 86400.0
+    t = np.arange(T) / max(T - 1, 1)
+    C = np.exp(rng.uniform(np.log(20), np.log(200), n_series))
+    r = rng.uniform(2.0, 8.0, n_series)
+    t0 = rng.uniform(0.2, 0.7, n_series)
+    ay = rng.uniform(0.05, 0.2, n_series)
+    aw = rng.uniform(0.05, 0.15, n_series)
+    ad = rng.uniform(0.0, 0.2, n_series)
+    ph = rng.uniform(0, 2 * np.pi, (n_series, 3))
+    lvl = C[:, None] / (1.0 + np.exp(-r[:, None] * (t[None, :] - t0[:, None])))
+    seas = ((1 + ay[:, None] * np.sin(2 * np.pi * d[None, :] / 365.25 + ph[:, :1]))
+            * (1 + aw[:, None] * np.sin(2 * np.pi * d[None, :] / 7.0 + ph[:, 1:2]))
+            * (1 + ad[:, None] * np.sin(2 * np.pi * d[None, :] + ph[:, 2:3])))
+    Y = np.maximum(0.0, lvl * seas + rng.normal(0.0, 1.0, (n_series, T)) * 0.05 * C[:, None])
+    cap = np.repeat((1.2 * Y.max(axis=1))[:, None], T, axis=1)
+    return Y, cap

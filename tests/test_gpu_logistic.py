@@ -1,0 +1,138 @@
+"""GPU parity for logistic growth (SURVEY.md §8a rows a4/a5/a7/a8, configs[4])
+and the sub-daily (yearly + weekly + daily) feature layout, against the CPU
+oracle (oracle/stan_lbfgs.c orc_objective: reverse mode through
+logistic_gamma; prophet_oracle.py: logistic_growth_init, piecewise_logistic).
+
+Logistic fits have no exact-MAP polish: they stop where Stan's L-BFGS stops,
+so the fitted objective is compared within Stan's stall band (1e-4 rel), and
+the forecast is checked against the oracle's predict at the GPU's own theta.
+"""
+import numpy as np
+import pytest
+import torch
+
+import distributed_forecasting_amd as dfa
+from distributed_forecasting_amd import synthetic
+from distributed_forecasting_amd.engine import ProphetConfig
+from oracle import prophet_oracle as po
+from oracle import stan_oracle as so
+
+pytestmark = pytest.mark.gpu
+
+DAILY_SEASONS = [("yearly", 365.25, 10), ("weekly", 7.0, 3)]
+HOURLY_SEASONS = [("yearly", 365.25, 10), ("weekly", 7.0, 3), ("daily", 1.0, 4)]
+
+
+def _cfg(seasons, growth):
+    cfg = dict(po.DEFAULT_CONFIG, growth=growth)
+    cfg["daily"] = (1.0, 4) if len(seasons) == 3 else None
+    return cfg
+
+
+def _engine(growth):
+    c = ProphetConfig.reference()
+    c.growth = growth
+    return dfa.Engine(0, c)
+
+
+def _dev(grid, A):
+    Yd = torch.zeros((A.shape[0], grid.T_pad), dtype=torch.float64, device="cuda")
+    Yd[:, :grid.T] = torch.from_numpy(A).cuda()
+    return Yd
+
+
+def _setup(ds, seasons, n, growth="logistic"):
+    eng = _engine(growth)
+    g = dfa.build_grid(ds, seasons, start_ns=int(ds[0]), t_scale_ns=int(ds[-1] - ds[0]))
+    Y, cap = synthetic.saturating_matrix(n, ds)
+    return eng, g, Y, cap
+
+
+@pytest.mark.parametrize("hourly", [False, True])
+@pytest.mark.parametrize("growth", ["logistic", "linear"])
+def test_objective_gradient(hourly, growth):
+    if not hourly and growth == "linear":
+        pytest.skip("covered by test_gpu_parity.test_objective_gradient")
+    ds = synthetic.hourly_dates(n_hours=24 * 90) if hourly else synthetic.daily_dates("2015-01-01", "2016-12-31")
+    seasons = HOURLY_SEASONS if hourly else DAILY_SEASONS
+    eng, g, Y, cap = _setup(ds, seasons, 4, growth)
+    capd = _dev(g, cap) if growth == "logistic" else None
+    _, ys, th0, _, cs = eng.prepare(g, _dev(g, Y), capd)
+    K, S = g.K, g.S
+    cfg = _cfg(seasons, growth)
+    rng = np.random.default_rng(1)
+    th = th0.cpu().numpy().copy()
+    for s in range(4):
+        st = po.build_problem(ds, Y[s], cfg, cap=cap[s] if growth == "logistic" else None)
+        assert np.allclose(th[s], st.theta0, rtol=1e-13, atol=1e-15)   # init (a4)
+    th[:, 2:2 + S] = rng.normal(0, 0.02, (4, S))
+    th[:, 3 + S:] = rng.normal(0, 0.05, (4, K))
+    th[:, 2 + S] = -1.5
+    f, gr = eng.objective_grad(g, ys, torch.from_numpy(th).cuda(), cs)
+    f, gr = f.cpu().numpy(), gr.cpu().numpy()
+    for s in range(4):
+        pb = po.build_problem(ds, Y[s], cfg, cap=cap[s] if growth == "logistic" else None).problem
+        fo, go, _ = so.objective(pb, th[s])
+        assert abs(f[s] - fo) <= 1e-12 * abs(fo)
+        assert np.max(np.abs(gr[s] - go)) <= 1e-10 * np.max(np.abs(go))
+
+
+def test_logistic_fit_and_forecast():
+    ds = synthetic.daily_dates("2015-01-01", "2016-12-31")
+    eng, g, Y, cap = _setup(ds, DAILY_SEASONS, 8)
+    cfg = _cfg(DAILY_SEASONS, "logistic")
+    fit = eng.fit(g, _dev(g, Y), cap=_dev(g, cap))
+    f = fit.f.cpu().numpy()
+    st = fit.status.cpu().numpy()
+    assert np.all(np.isin(st, [0, 10, 20, 21, 30, 31]))      # Stan's own termination
+    fut = dfa.future_dates(ds, 90)
+    fg = eng.predict_grid(fit, fut)
+    capf = np.repeat(cap[:, :1], len(fut), axis=1)
+    out = eng.predict(fit, fg, seed=3, cap=_dev(fg, capf))
+    th = fit.theta.cpu().numpy()
+    for s in range(8):
+        setup = po.build_problem(ds, Y[s], cfg, cap=cap[s])
+        _, fo, *_ = so.fit_setup(setup)
+        # Stan-faithful on both sides, so compared within Stan's own stall
+        # band: perturbing the oracle's init by 1e-13 moves its logistic
+        # endpoint by up to 9e-4 relative (4e-5 for linear growth)
+        assert f[s] <= fo + 2e-3 * abs(fo)
+        par = po.params_from_theta(th[s], setup.problem.S)
+        pt = po.predict_point(setup, par, fut, cfg, cap=capf[s])
+        ysc = setup.hist.y_scale
+        yh = out["yhat"][s, :fg.T].double().cpu().numpy()
+        assert np.max(np.abs(yh - pt["yhat"])) <= 1e-5 * ysc
+        tr = out["trend"][s, :fg.T].double().cpu().numpy()
+        assert np.max(np.abs(tr - pt["trend"])) <= 1e-5 * ysc
+        lo = out["yhat_lower"][s, :fg.T].cpu().numpy()
+        hi = out["yhat_upper"][s, :fg.T].cpu().numpy()
+        assert np.all(np.isfinite(lo)) and np.all(np.isfinite(hi))
+        assert np.all(lo <= yh + 1e-3 * ysc) and np.all(hi >= yh - 1e-3 * ysc)
+        # future trend band opens up and stays below the capacity
+        tlo = out["trend_lower"][s, :fg.T].cpu().numpy()
+        thi = out["trend_upper"][s, :fg.T].cpu().numpy()
+        assert thi[-1] - tlo[-1] > 0.0
+        assert np.all(thi <= capf[s] * (1 + 1e-6))
+
+
+def test_logistic_intervals_vs_oracle_sampler():
+    """Future-row trend bands: GPU Monte-Carlo vs the oracle's literal
+    per-sample loop (Poisson changepoints, Laplace deltas, logistic_gamma over
+    the concatenated changepoints), same theta; widths agree within MC error."""
+    ds = synthetic.daily_dates("2015-01-01", "2016-12-31")
+    eng, g, Y, cap = _setup(ds, DAILY_SEASONS, 4)
+    cfg = _cfg(DAILY_SEASONS, "logistic")
+    fit = eng.fit(g, _dev(g, Y), cap=_dev(g, cap))
+    fut = dfa.future_dates(ds, 90)
+    fg = eng.predict_grid(fit, fut)
+    capf = np.repeat(cap[:, :1], len(fut), axis=1)
+    out = eng.predict(fit, fg, seed=9, cap=_dev(fg, capf))
+    th = fit.theta.cpu().numpy()
+    for s in range(4):
+        setup = po.build_problem(ds, Y[s], cfg, cap=cap[s])
+        par = po.params_from_theta(th[s], setup.problem.S)
+        o = po.sample_uncertainty(setup, par, fut, n_samples=1000, cfg=cfg, cap=capf[s],
+                                  rng=np.random.default_rng(s))
+        w_o = o["yhat_upper"][-1] - o["yhat_lower"][-1]
+        w_g = float(out["yhat_upper"][s, fg.T - 1] - out["yhat_lower"][s, fg.T - 1])
+        assert 0.6 * w_o < w_g < 1.6 * w_o

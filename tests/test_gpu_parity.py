@@ -72,7 +72,7 @@ def test_grid_irregular_dates(eng):
 def test_objective_gradient(eng, golden_ref):
     ds, Y = golden_ref["ds_ns"], golden_ref["Y"]
     g = _grid(eng, ds)
-    _, ys, th0, _ = eng.prepare(g, _Y(g, Y))
+    _, ys, th0, _, _ = eng.prepare(g, _Y(g, Y))
     assert np.array_equal(th0.cpu().numpy(), golden_ref["theta0"])
     rng = np.random.default_rng(0)
     th = golden_ref["theta0"].copy()

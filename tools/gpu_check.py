@@ -31,7 +31,7 @@ print("seg ok:", np.array_equal(seg, pb.A.sum(1).astype(int)))
 
 Yd = torch.zeros((n, grid.T_pad), dtype=torch.float64, device="cuda")
 Yd[:, :grid.T] = torch.from_numpy(Y).cuda()
-y_scale, y_scaled, theta0, status = eng.prepare(grid, Yd)
+y_scale, y_scaled, theta0, status, _ = eng.prepare(grid, Yd)
 torch.cuda.synchronize()
 print("y_scale ok:", np.allclose(y_scale.cpu().numpy(), np.abs(Y).max(1)))
 print("theta0 diff:", np.abs(theta0[0].cpu().numpy() - setup.theta0).max())

@@ -15,7 +15,7 @@ grid = dfa.build_grid(ds, seasons, start_ns=int(ds[0]), t_scale_ns=int(ds[-1] - 
 Yd = torch.zeros((n, grid.T_pad), dtype=torch.float64, device="cuda")
 Yd[:, :grid.T] = torch.from_numpy(Y).cuda()
 fut = dfa.future_dates(ds, 90)
-y_scale, y_scaled, theta0, status = eng.prepare(grid, Yd)
+y_scale, y_scaled, theta0, status, _ = eng.prepare(grid, Yd)
 for r in range(3):
     torch.cuda.synchronize(); t0 = time.time()
     f_, g_ = eng.objective_grad(grid, y_scaled, theta0)
