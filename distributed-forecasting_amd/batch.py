@@ -149,6 +149,17 @@ class GridSpec:
     t_change: torch.Tensor
 
 
+def _dense(A, n: int, T: int, T_pad: int, dev) -> torch.Tensor:
+    """[n, T] numpy/tensor -> zero-padded [n, T_pad] float64 device tensor."""
+    out = torch.zeros((n, T_pad), dtype=torch.float64, device=dev)
+    if isinstance(A, torch.Tensor):
+        out[:, :T] = A[:, :T].to(dev, torch.float64)
+    else:
+        out[:, :T] = torch.from_numpy(np.array(np.broadcast_to(
+            np.asarray(A, np.float64), (n, T)))).to(dev)
+    return out
+
+
 class FittedBatch:
     """n series fitted on one shared grid (all tensors on one GPU)."""
 
@@ -169,7 +180,7 @@ class FittedBatch:
 
     @classmethod
     def fit_dense(cls, engine: E.Engine, fit_ds: np.ndarray, Y, history_dates=None,
-                  series_ids=None, polish: bool = True, seasons=None) -> "FittedBatch":
+                  series_ids=None, polish: bool = True, seasons=None, cap=None) -> "FittedBatch":
         """Fit every row of Y ([n, T] numpy or device tensor, raw y) on the
         sorted date grid ``fit_ds`` (K1 grid + K2/K3 fit).  ``seasons``
         overrides the auto rules (CV folds reuse the parent's seasonalities,
@@ -194,7 +205,12 @@ class FittedBatch:
             Yd[:, :T] = Y[:, :T].to(dev, torch.float64)
         else:
             Yd[:, :T] = torch.from_numpy(np.ascontiguousarray(Y, dtype=np.float64)).to(dev)
-        fit = engine.fit(grid, Yd, polish=polish)
+        capd = None
+        if cfg.growth == "logistic":
+            if cap is None:
+                raise ValueError('Capacities must be supplied for logistic growth in column "cap"')
+            capd = _dense(cap, n, T, grid.T_pad, dev)
+        fit = engine.fit(grid, Yd, polish=polish, cap=capd)
         hd = fit_ds if history_dates is None else history_dates
         return cls(engine, fit, np.unique(hd), fit_ds, series_ids)
 
@@ -203,13 +219,20 @@ class FittedBatch:
         return GridSpec(list(g.seasons), int(g.start_ns), int(g.t_scale_ns), g.t_change)
 
     def predict(self, ds_ns: np.ndarray, *, seed: int = 0, n_samples: int | None = None,
-                components: bool = True):
+                components: bool = True, cap=None):
         """Forecast every series of the batch on the dates ``ds_ns`` (sorted).
-        Returns (T, dict of float32 device tensors [n, T_pad])."""
+        ``cap`` ([n, T] capacities on those dates) is required for logistic
+        growth.  Returns (T, dict of float32 device tensors [n, T_pad])."""
         ds_ns = np.asarray(ds_ns, np.int64)
         fg = self.engine.predict_grid(self.fit, ds_ns)
+        capd = None
+        if self.engine.config.growth == "logistic":
+            if cap is None:
+                raise ValueError('Capacities must be supplied for logistic growth in column "cap"')
+            n = int(self.fit.theta.shape[0])
+            capd = _dense(cap, n, fg.T, fg.T_pad, torch.device("cuda", self.engine.device))
         out = self.engine.predict(self.fit, fg, n_samples=n_samples, seed=seed,
-                                  components=components, series_id=self.series_ids)
+                                  components=components, series_id=self.series_ids, cap=capd)
         return fg.T, out
 
     # -------------------------------------------------------- params store

@@ -9,10 +9,11 @@ calls ``predict`` on a loaded model, model_wrapper.py:58-61).  This class keeps
 that surface; ``fit`` is a batch of one through the same kernels the batched
 entry points use.
 
-Supported: linear and flat growth, auto/True/False/int seasonalities
+Supported: linear, flat and logistic growth (capacity column 'cap', floor 0),
+auto/True/False/int seasonalities
 (yearly, weekly, daily), additive and multiplicative seasonality, MAP fit,
 ``uncertainty_samples`` up to 1024.  Not supported yet (raise
-NotImplementedError): logistic growth, holidays, extra regressors, custom
+NotImplementedError): logistic floor, holidays, extra regressors, custom
 seasonalities, user-specified changepoints, ``mcmc_samples > 0``.
 """
 from __future__ import annotations
@@ -64,8 +65,6 @@ class Prophet:
                  uncertainty_samples=1000, stan_backend=None, *, device=None, seed=0):
         if growth not in ("linear", "flat", "logistic"):
             raise ValueError('Parameter "growth" should be "linear", "logistic" or "flat".')
-        if growth == "logistic":
-            raise NotImplementedError("logistic growth is not supported on the GPU path yet")
         if changepoints is not None:
             raise NotImplementedError("user-specified changepoints are not supported yet")
         if holidays is not None:
@@ -140,9 +139,20 @@ class Prophet:
             raise ValueError("Found infinity in column y.")
         order = np.argsort(ds, kind="stable")
         ds, y = ds[order], y[order]
+        cap = None
+        if self.growth == "logistic":
+            # UPSTREAM setup_dataframe: capacities are required; floor is not
+            # supported on this path (logistic_floor = False)
+            if "cap" not in history:
+                raise ValueError('Capacities must be supplied for logistic growth in column "cap"')
+            if "floor" in history:
+                raise NotImplementedError("logistic floor is not supported on the GPU path")
+            cap = history["cap"].to_numpy(np.float64)[order][None, :]
+            if np.any(cap <= 0.0):
+                raise ValueError("Cap must be greater than floor (which defaults to 0).")
         eng = get_engine(self.config(), self.device)
         fb = B.FittedBatch.fit_dense(eng, ds, y[None, :], history_dates=all_ds,
-                                     series_ids=np.array([0], np.int32))
+                                     series_ids=np.array([0], np.int32), cap=cap)
         self._attach(fb, history=history.iloc[order].reset_index(drop=True))
         self.fit_kwargs = dict(kwargs)
         return self
@@ -184,6 +194,8 @@ class Prophet:
             h["floor"] = 0.0
             h["t"] = (B.to_ns(h["ds"]) - int(g.start_ns)) / float(int(g.t_scale_ns))
             h["y_scaled"] = h["y"] / self.y_scale
+            if "cap" in h:
+                h["cap_scaled"] = h["cap"] / self.y_scale
             self.history = h
         else:
             self.history = pd.DataFrame({"ds": self.history_dates})
@@ -207,26 +219,35 @@ class Prophet:
         if self._batch is None:
             raise Exception("Model has not been fit.")
         if df is None:
-            ds = B.to_ns(self.history["ds"])
-        else:
-            if df.shape[0] == 0:
-                raise ValueError("Dataframe has no rows.")
-            if "ds" not in df:
-                raise ValueError('Dataframe must have column "ds".')
-            ds = B.to_ns(df["ds"])
-        ds = np.sort(ds, kind="stable")
+            df = self.history
+        if df.shape[0] == 0:
+            raise ValueError("Dataframe has no rows.")
+        if "ds" not in df:
+            raise ValueError('Dataframe must have column "ds".')
+        ds = B.to_ns(df["ds"])
+        order = np.argsort(ds, kind="stable")
+        ds = ds[order]
+        cap = None
+        if self.growth == "logistic":
+            if "cap" not in df:
+                raise ValueError('Capacities must be supplied for logistic growth in column "cap"')
+            cap = df["cap"].to_numpy(np.float64)[order]
         return predict_frame(self._batch, 0, ds, self.seasonality_mode, seed=self.seed,
-                             n_samples=int(self.uncertainty_samples or 0))
+                             n_samples=int(self.uncertainty_samples or 0), cap=cap)
 
 
 def predict_frame(fb: B.FittedBatch, row: int, ds: np.ndarray, mode: str, seed: int = 0,
-                  n_samples: int = 1000, out=None, Tf=None) -> pd.DataFrame:
-    """Prophet-1.0 column layout for series ``row`` of a fitted batch."""
+                  n_samples: int = 1000, out=None, Tf=None, cap=None) -> pd.DataFrame:
+    """Prophet-1.0 column layout for series ``row`` of a fitted batch
+    (logistic growth: ``cap`` on the sorted dates, echoed after 'trend')."""
     if out is None:
-        Tf, out = fb.predict(ds, seed=seed, n_samples=n_samples, components=True)
+        Tf, out = fb.predict(ds, seed=seed, n_samples=n_samples, components=True,
+                             cap=None if cap is None else np.asarray(cap)[None, :])
     host = {k: v[row, :Tf].cpu().numpy() for k, v in out.items()}
     names = [s[0] for s in fb.fit.grid.seasons]
     cols = {"ds": ds.astype("datetime64[ns]"), "trend": host["trend"]}
+    if cap is not None:
+        cols["cap"] = np.asarray(cap, np.float64)
     cols["yhat_lower"] = host["yhat_lower"]
     cols["yhat_upper"] = host["yhat_upper"]
     cols["trend_lower"] = host["trend_lower"]

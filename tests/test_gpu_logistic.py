@@ -136,3 +136,32 @@ def test_logistic_intervals_vs_oracle_sampler():
         w_o = o["yhat_upper"][-1] - o["yhat_lower"][-1]
         w_g = float(out["yhat_upper"][s, fg.T - 1] - out["yhat_lower"][s, fg.T - 1])
         assert 0.6 * w_o < w_g < 1.6 * w_o
+
+
+def test_prophet_class_logistic():
+    """Host surface: Prophet(growth='logistic') with a 'cap' column (UPSTREAM
+    setup_dataframe) runs the same kernels as the batched engine; the forecast
+    matches the oracle's predict at the fitted theta, and 'cap' is echoed."""
+    import pandas as pd
+    ds = synthetic.daily_dates("2015-01-01", "2016-12-31")
+    Y, cap = synthetic.saturating_matrix(1, ds)
+    df = pd.DataFrame({"ds": ds.astype("datetime64[ns]"), "y": Y[0], "cap": cap[0]})
+    m = dfa.Prophet(growth="logistic", seasonality_mode="multiplicative",
+                    yearly_seasonality=True, weekly_seasonality=True, daily_seasonality=False)
+    m.fit(df)
+    fut = m.make_future_dataframe(periods=90)
+    with pytest.raises(ValueError, match="Capacities must be supplied"):
+        m.predict(fut)
+    fut["cap"] = cap[0, 0]
+    fc = m.predict(fut)
+    assert list(fc.columns[:3]) == ["ds", "trend", "cap"]
+    assert np.allclose(fc["cap"], cap[0, 0])
+    cfg = _cfg(DAILY_SEASONS, "logistic")
+    setup = po.build_problem(ds, Y[0], cfg, cap=cap[0])
+    th = m._batch.fit.theta[0].cpu().numpy()
+    pt = po.predict_point(setup, po.params_from_theta(th, setup.problem.S),
+                          dfa.future_dates(ds, 90), cfg, cap=fut["cap"].to_numpy())
+    ysc = setup.hist.y_scale
+    assert np.max(np.abs(fc["yhat"].to_numpy() - pt["yhat"])) <= 1e-5 * ysc
+    assert np.all(fc["trend"].to_numpy() <= fut["cap"].to_numpy() * (1 + 1e-6))
+    assert "cap_scaled" in m.history

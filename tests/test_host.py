@@ -50,6 +50,16 @@ def test_no_cpu_fallback_without_gpu():
         dfa.Prophet().fit(df[["ds", "y"]])
 
 
+def test_logistic_requires_cap():
+    # UPSTREAM setup_dataframe: raised before any GPU work
+    df = synthetic.store_item_frame(1, 1, "2017-01-01", "2017-03-01")
+    with pytest.raises(ValueError, match="Capacities must be supplied"):
+        dfa.Prophet(growth="logistic").fit(df[["ds", "y"]])
+    d2 = df[["ds", "y"]].assign(cap=100.0, floor=0.0)
+    with pytest.raises(NotImplementedError, match="floor"):
+        dfa.Prophet(growth="logistic").fit(d2)
+
+
 def test_seasonality_auto_rules():
     cfg = ProphetConfig()
     d = NS_PER_DAY
