@@ -11,6 +11,7 @@ SOURCES = [os.path.join(_HERE, "csrc", "pf_engine.hip")]
 DEPS = SOURCES + [os.path.join(_HERE, "csrc", "pf_common.h"),
                   os.path.join(_HERE, "csrc", "pf_polish.h"),
                   os.path.join(_HERE, "csrc", "pf_cv.h"),
+                  os.path.join(_HERE, "csrc", "pf_ostat.h"),
                   os.path.join(_ROOT, "include", "prophet_hip.h")]
 OUT = os.path.join(_HERE, "libprophet_hip.so")
 ARCH = os.environ.get("PF_OFFLOAD_ARCH", "gfx950")

@@ -9,7 +9,9 @@
 //      accumulated on FP64 MFMA (v_mfma_f64_16x16x4f64);
 //   2. the lasso-QP subproblem min gh.d + d'Hd/2 + c||x_delta + d_delta||_1,
 //      solved exactly by an active-set method (Cholesky solves in LDS, wave 0);
-//   3. Armijo backtracking on the true objective (collective evaluations).
+//   3. Armijo backtracking on the true objective (collective evaluations);
+//   4. after a full step the next QP reuses H and its swept matrix (lagged
+//      Hessian, see polish_run).
 // Same algorithm as oracle/stan_lbfgs.c:orc_polish (the CPU check).
 // Linear growth, K <= 32, 2 + S <= 32 (the reference configuration).
 #pragma once
@@ -80,6 +82,8 @@ __device__ __forceinline__ void hessian_collective(const FitKArgs &a, FitSmem<NW
   Q = wave_sum(Q);
   if (lane == 0) sm.rrw[wave] = Q;
   __syncthreads();
+  PF_STAMP(13);
+  PF_COUNT(15);
   // ---- H2: J^T J - R on FP64 MFMA.  k-steps of 4 rows, split over waves.
   pf_d4 acc[PF_NTILE];
 #pragma unroll
@@ -138,6 +142,7 @@ __device__ __forceinline__ void hessian_collective(const FitKArgs &a, FitSmem<NW
     acc[8] = __builtin_amdgcn_mfma_f64_16x16x4f64(D1, W2, acc[8], 0, 0, 0);
     acc[9] = __builtin_amdgcn_mfma_f64_16x16x4f64(D1, W3, acc[9], 0, 0, 0);
   }
+  PF_STAMP(14);
   // ---- H3: chained reduction of the tiles over waves through one
   // wave-sized LDS buffer (NW-1 hops; keeps the union region small)
   double *red = sm.U;  // [PF_NTILE][4][64]
@@ -332,25 +337,37 @@ __device__ __forceinline__ double wave_symv(const double *A, int LD, int P, cons
 
 // Active-set solution of min gh.(z-x) + (z-x)'H(z-x)/2 + c||z_delta||_1 (wave 0).
 // Returns z in lane p; false if a pivot failed or the active set did not settle.
+//
+// Cold start (warm = false): the starting active set is {delta: |gh| <= c}
+// and A holds H with its complement swept in (sweep_in_free).  Warm start:
+// A and the active set (zero, sgn_: lane-local, wave 0) are the ones the
+// previous QP ended with — the swept matrix depends only on H and the free
+// set, so a QP at a new (x, gh) under the same H needs no initial sweeps.
 template <int NW, int KMAX, int MODE>
 __device__ __forceinline__ bool qp_active(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, double x, double gh, double c,
-                          double &z, int &nsolve) {
+                          double &z, int &nsolve, bool &zero, double &sgn_, bool warm) {
   const int lane = pf_lane();
   const int P = a.P, S = a.S, LD = sm.LD;
-  const double *H = sm.U;
   double *A = sm.U + (size_t)P * LD;
   const bool isd = (lane >= 2 && lane < 2 + S);
-  bool zero = false;
-  double sgn_ = 0.0;
   if (isd) {
     const double sgx = (x > 0.0) - (x < 0.0), sgg = (gh > 0.0) - (gh < 0.0);
-    if (fabs(gh) <= c) zero = true;
-    else if (x != 0.0 && sgx == -sgg) sgn_ = sgx;
-    else sgn_ = -sgg;
+    if (!warm) {
+      zero = false;
+      sgn_ = 0.0;
+      if (fabs(gh) <= c) zero = true;
+      else if (x != 0.0 && sgx == -sgg) sgn_ = sgx;
+      else sgn_ = -sgg;
+    } else if (!zero) {
+      sgn_ = (x != 0.0) ? sgx : -sgg;
+    }
+  } else {
+    zero = false;
+    sgn_ = 0.0;
   }
-  // A already holds H with every initially free coordinate swept in
+  // cold: A holds H with every initially free coordinate swept in
   // (sweep_in_free, all waves); a failed pivot there leaves flag[1] set
-  if (sm.flag[1]) return false;
+  if (!warm && sm.flag[1]) return false;
   z = x;
   const int max_as = 2 * S + 16;
   for (int it = 0; it < max_as; ++it) {
@@ -407,7 +424,17 @@ __device__ __forceinline__ bool qp_active(const FitKArgs &a, FitSmem<NW, KMAX, M
 }
 
 // Returns true when the polish certifies the optimum: the last lasso-QP
-// (exact Hessian, solved to KKT) predicts no decrease beyond 1e-15 |f|.
+// (solved to KKT) predicts no decrease beyond 1e-15 |f|.
+//
+// Lagged Hessian: after a full Newton step (alpha = 1) the next QP reuses the
+// Hessian and the swept matrix of the previous one (warm start) instead of
+// recomputing them, as long as each lagged step shrinks the predicted
+// decrease by >= 100x (superlinear); otherwise, or after a backtracked step or
+// a failed warm QP, the exact Hessian is recomputed.  A QP under any positive
+// definite model predicts zero decrease exactly at a KKT point, so the
+// certificate is unchanged; oracle/stan_lbfgs.c:orc_polish recomputes every
+// iteration and reaches the same MAP.
+#define PF_POLISH_MAXLAG 4
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
 __device__ __forceinline__ bool polish_run(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, double &x, double &f,
                            double &g, int &n_eval, int &n_newton) {
@@ -418,18 +445,27 @@ __device__ __forceinline__ bool polish_run(const FitKArgs &a, FitSmem<NW, KMAX, 
   double *ws = a.ws + (size_t)blockIdx.x * 3 * a.Tp;
   n_newton = 0;
   bool cert = false;
+  bool need_h = true;
+  int lag = 0;
+  double dec_prev = 0.0;
+  bool zero = false;    // QP active set (wave 0, lane = parameter)
+  double sgn_ = 0.0;
   for (int it = 0; it < a.o.polish_max_iter; ++it) {
     const double gh = isd ? g - c * (double)((x > 0.0) - (x < 0.0)) : g;
-    PF_STAMP(20);
-    hessian_collective<NW, KMAX, O0, O1, O2, MODE>(a, sm, x, gh, ws);
-    __syncthreads();
-    PF_STAMP(21);
-    sweep_in_free<NW, KMAX, MODE>(a, sm, gh, c);
-    PF_STAMP(24);
+    const bool fresh = need_h;
+    if (fresh) {
+      PF_STAMP(20);
+      hessian_collective<NW, KMAX, O0, O1, O2, MODE>(a, sm, x, gh, ws);
+      __syncthreads();
+      PF_STAMP(21);
+      sweep_in_free<NW, KMAX, MODE>(a, sm, gh, c);
+      PF_STAMP(24);
+    }
+    PF_STAMP(19);
     if (wave == 0) {
       double z;
       int ns = 0;
-      const bool ok = qp_active<NW, KMAX, MODE>(a, sm, x, gh, c, z, ns);
+      const bool ok = qp_active<NW, KMAX, MODE>(a, sm, x, gh, c, z, ns, zero, sgn_, !fresh);
       PF_STAMP(22);
       const double d = (lane < a.P) ? z - x : 0.0;
       double dec = wave_sum(gh * d);
@@ -443,11 +479,20 @@ __device__ __forceinline__ bool polish_run(const FitKArgs &a, FitSmem<NW, KMAX, 
     const bool qp_ok = sm.fout[3] != 0.0;
     const double d = sm.pd[lane];
     __syncthreads();
+    if (!fresh && (!qp_ok || !(fabs(dec) < 1e-2 * fabs(dec_prev)))) {
+      // warm QP failed or the lagged model stopped converging fast:
+      // recompute the Hessian at the same point
+      need_h = true;
+      lag = 0;
+      continue;
+    }
     if (!(dec < -1e-15 * fabs(f))) {
       cert = qp_ok && dec == dec;
       break;
     }
     ++n_newton;
+    PF_COUNT(18);
+    PF_STAMP(16);
     double alpha = 1.0, fn = 0.0, gn = 0.0, xn = x;
     bool acc = false;
     for (int ls = 0; ls < 30; ++ls) {
@@ -457,11 +502,14 @@ __device__ __forceinline__ bool polish_run(const FitKArgs &a, FitSmem<NW, KMAX, 
       if (!bad && fn <= f + 1e-4 * alpha * dec) { acc = true; break; }
       alpha *= 0.5;
     }
-    PF_STAMP(23);
+    PF_STAMP(17);
     if (!acc) break;
     x = xn;
     f = fn;
     g = gn;
+    need_h = !(alpha == 1.0 && lag < PF_POLISH_MAXLAG);
+    lag = need_h ? 0 : lag + 1;
+    dec_prev = dec;
   }
   return cert;
 }

@@ -42,5 +42,6 @@ t0 = time.time(); fit = eng.fit(grid, Yd); torch.cuda.synchronize(); dt = time.t
 lib.pf_debug_stamps(buf, 1)
 v = np.array(list(buf), dtype=np.float64)
 print(f"default fit {dt*1e3:.2f} ms; series0 n_eval={fit.n_eval[0].item()} status={fit.status[0].item()}")
-print(f"   polish: hessian {(v[21]-v[20]):.0f}  qp {(v[22]-v[21]):.0f}  line search {(v[23]-v[22]):.0f} cycles (total over Newton steps)")
-print(f"   qp: initial sweeps {v[26]:.0f} (to stamp24 {(v[24]-v[21]):.0f} cycles)  iterations {v[27]:.0f}  symv {(v[29]-v[28]):.0f}  rev-sweeps {(v[31]-v[30]):.0f} cycles")
+nh = max(v[15], 1)
+print(f"   polish: {v[15]:.0f} Hessians: total {(v[21]-v[20])/nh:.0f}/Hessian (H1 rows {(v[13]-v[20])/nh:.0f}, H2 MFMA {(v[14]-v[13])/nh:.0f}, H3+H4 {(v[21]-v[14])/nh:.0f}); initial sweeps {(v[24]-v[21]):.0f} total; qp {(v[22]-v[19]):.0f} total; line search {(v[17]-v[16]):.0f} total cycles")
+print(f"   qp: initial sweeps {v[26]:.0f}  iterations {v[27]:.0f}  symv {(v[29]-v[28]):.0f}  rev-sweeps {(v[31]-v[30]):.0f} cycles; Newton steps (block 0) {v[18]:.0f}")
