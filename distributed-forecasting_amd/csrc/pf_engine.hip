@@ -62,7 +62,13 @@ __device__ unsigned long long pf_dbg[32];
   do {                                                                           \
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&pf_dbg[i], 1ull);        \
   } while (0)
+#define PF_STAMP1(i)                                                             \
+  do {                                                                           \
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)                  \
+      atomicAdd(&pf_dbg[i], (unsigned long long)__builtin_amdgcn_s_memtime());   \
+  } while (0)
 #else
+#define PF_STAMP1(i) do { } while (0)
 #define PF_STAMP(i) do { } while (0)
 #define PF_COUNT(i) do { } while (0)
 #endif
@@ -1478,61 +1484,6 @@ struct PredKArgs {
   const double *cap;          // [n][Tp] logistic capacity / y_scale on the predicted rows
 };
 
-// k-th and (k+1)-th smallest of the wave's samples (v[q] = +inf if absent).
-// Fast path: bound from the (k+2)-th smallest per-lane minimum, compact the
-// candidates into LDS, bitonic-sort 64.  Fallback: exact bit-bisection.
-__device__ __forceinline__ void wave_select_pair(const float (&v)[PF_NQ], int k, float *buf, float &a, float &b) {
-  const int lane = pf_lane();
-  float lmin = INFINITY;
-#pragma unroll
-  for (int q = 0; q < PF_NQ; ++q) lmin = fminf(lmin, v[q]);
-  int M = 1 << 30;
-  if (k + 1 < 63) {
-    const float srt = wave_bitonic_sort_asc(lmin);
-    const float U = readlane_f32(srt, k + 1);
-    int base = 0;
-    const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-#pragma unroll
-    for (int q = 0; q < PF_NQ; ++q) {
-      const bool pr = v[q] <= U;
-      const unsigned long long m = __ballot(pr);
-      if (pr) {
-        const int pos = base + __popcll(m & lt);
-        if (pos < 64) buf[pos] = v[q];
-      }
-      base += __popcll(m);
-    }
-    M = base;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    if (M <= 64) {
-      float c = (lane < M) ? buf[lane] : INFINITY;
-      c = wave_bitonic_sort_asc(c);
-      a = readlane_f32(c, k);
-      b = readlane_f32(c, k + 1);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-  }
-  if (M > 64) {
-    uint32_t key[PF_NQ];
-#pragma unroll
-    for (int q = 0; q < PF_NQ; ++q) key[q] = pf_f2ord(v[q]);
-    for (int want = 0; want < 2; ++want) {
-      const int kk = k + want;
-      uint32_t lo = 0u, hi = 0xFFFFFFFFu;
-      while (lo < hi) {
-        const uint32_t mid = lo + ((hi - lo) >> 1);
-        int cnt = 0;
-#pragma unroll
-        for (int q = 0; q < PF_NQ; ++q) cnt += __popcll(__ballot(key[q] <= mid));
-        if (cnt >= kk + 1) hi = mid; else lo = mid + 1;
-      }
-      if (want == 0) a = pf_ord2f(lo); else b = pf_ord2f(lo);
-    }
-  }
-}
-
 // numpy _lerp: a + (b-a)*t, or b - (b-a)*(1-t) when t >= 0.5
 __device__ __forceinline__ float np_lerp(float a, float b, float t) {
   const float d = b - a;
@@ -1665,235 +1616,7 @@ __global__ __launch_bounds__(256) void k_predict_det(PredKArgs a) {
   if (a.tr) { a.trlo[o] = (float)trend; a.trhi[o] = (float)trend; }
 }
 
-// ---- K5: Monte-Carlo rows.  Grid (G, n_series), 4 waves per block, wave per
-// row (rows r0 + w, r0 + w + 4G, ...).  r0 = first random-trend row (exact)
-// or 0 (sample).  Each block first draws every sample's future changepoints
-// once (Poisson count, uniform times on (1, T], Laplace(λ) rates) into LDS,
-// so a row's 1000 trend offsets cost ~1.2 FMAs each; a sample with more than
-// PF_MC_NCP changepoints (P ≈ 3e-4 at T=1826) re-derives them from its
-// counter-based stream (same draws, evaluated in fp64).
-#define PF_MC_NCP 6
-#define PF_MC_WAVES_PER_SERIES 16
-#define PF_MC_WPB 8  // waves per block (VGPR budget: 2 waves/SIMD)
-
-__device__ __forceinline__ void mc_sample_cp(uint32_t seed0, uint32_t seed1, uint32_t series, int smp,
-                                             int c, double t_max, double lam, double &tc, double &dl) {
-  const pf_u4 rc = philox4x32_10(pf_u4{(uint32_t)smp, (uint32_t)(c + 1), (uint32_t)series, 0x7EE2D00Du},
-                                 seed0 ^ 0x5A5A5A5Au, seed1);
-  tc = 1.0 + pf_u01d(rc.x, rc.y) * (t_max - 1.0);
-  const double ul = pf_u01d(rc.z, rc.w);
-  dl = (ul >= 0.5) ? -lam * log(2.0 - ul - ul) : lam * log(ul + ul);
-}
-
-__device__ __forceinline__ int mc_sample_count(uint32_t seed0, uint32_t seed1, uint32_t series, int smp,
-                                               double lam_pois, double e_neg) {
-  const pf_u4 r0 = philox4x32_10(pf_u4{(uint32_t)smp, 0u, (uint32_t)series, 0x7EE2D00Du},
-                                 seed0 ^ 0x5A5A5A5Au, seed1);
-  // Poisson(lam_pois) by inversion
-  const double u0 = pf_u01d(r0.x, r0.y);
-  int n = 0;
-  if (lam_pois > 0.0) {
-    double p = e_neg, F = p;
-    while (u0 > F && n < 100000) {
-      ++n;
-      p *= lam_pois / (double)n;
-      F += p;
-      if (p == 0.0 && F < u0) break;
-    }
-  }
-  return n;
-}
-
-__device__ __noinline__ double mc_offset_slow(uint32_t seed0, uint32_t seed1, uint32_t series, int smp,
-                                              int n, double t_max, double lam, double ti) {
-  double off = 0.0;
-  for (int c = 0; c < n; ++c) {
-    double tc, dl;
-    mc_sample_cp(seed0, seed1, series, smp, c, t_max, lam, tc, dl);
-    if (ti >= tc) off += dl * (ti - tc);
-  }
-  return off;
-}
-
-// logistic trend sample (scaled units, without cap) at ti: walk the
-// sample's new changepoints in time order from the last fitted segment
-// (UPSTREAM piecewise_logistic over the concatenated changepoints)
-__device__ __noinline__ double mc_logistic_slow(uint32_t seed0, uint32_t seed1, uint32_t series, int smp,
-                                                int n, double t_max, double lam, double ti, double k0,
-                                                double m0) {
-  double tcs[32], dls[32];
-  const int nn = n < 32 ? n : 32;
-  for (int c = 0; c < nn; ++c) {
-    double tc, dl;
-    mc_sample_cp(seed0, seed1, series, smp, c, t_max, lam, tc, dl);
-    int q = c;
-    while (q > 0 && tcs[q - 1] > tc) { tcs[q] = tcs[q - 1]; dls[q] = dls[q - 1]; --q; }
-    tcs[q] = tc;
-    dls[q] = dl;
-  }
-  double kc = k0, mc = m0;
-  for (int c = 0; c < nn && ti >= tcs[c]; ++c) {
-    const double kn = kc + dls[c];
-    mc = mc + (tcs[c] - mc) * (1.0 - kc / kn);
-    kc = kn;
-  }
-  return 1.0 / (1.0 + exp(-(kc * (ti - mc))));
-}
-
-template <int KMAX, int WPB>
-__global__ __launch_bounds__(WPB * 64) void k_predict_mc(PredKArgs a) {
-  __shared__ PredSeries ps;
-  __shared__ float2 s_cp[PF_MC_NCP][64 * PF_NQ];   // (t_c, delta) per sample
-  __shared__ int s_cnt[64 * PF_NQ];
-  __shared__ float s_buf[WPB][64];
-  __shared__ int s_r0;
-  const int series = blockIdx.y, lane = pf_lane(), wave = pf_wave();
-  const uint32_t sid = a.series_id ? a.series_id[series] : (uint32_t)series;
-  pred_setup(a, series, ps);
-  const double t_max = a.t[a.Tf - 1];
-  if (threadIdx.x == 0) {
-    int r0 = 0;
-    if (a.method != PF_INTERVAL_SAMPLE) {
-      // first random-trend row (rows sorted by t)
-      int lo = 0, hi = a.Tf;
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (pred_row_random(a, a.t[mid], t_max)) hi = mid; else lo = mid + 1;
-      }
-      r0 = lo;
-    }
-    s_r0 = r0;
-  }
-  __syncthreads();
-  const int r0 = s_r0;
-  if (r0 >= a.Tf) return;
-  const double sigma = ps.sigma, ysc = ps.ysc, lam = ps.lam;
-  const bool any_random = pred_row_random(a, t_max, t_max);
-  const double lam_pois = any_random ? (double)a.S * (t_max - 1.0) : 0.0;
-  if (any_random) {
-    const double e_neg = exp(-lam_pois);
-    for (int smp = threadIdx.x; smp < a.N; smp += WPB * 64) {
-      const int n = mc_sample_count(a.seed0, a.seed1, sid, smp, lam_pois, e_neg);
-      s_cnt[smp] = n;
-      for (int c = 0; c < n && c < PF_MC_NCP; ++c) {
-        double tc, dl;
-        mc_sample_cp(a.seed0, a.seed1, sid, smp, c, t_max, lam, tc, dl);
-        // kept in time order (logistic walks them in order; linear sums)
-        int q = c;
-        while (q > 0 && s_cp[q - 1][smp].x > (float)tc) { s_cp[q][smp] = s_cp[q - 1][smp]; --q; }
-        s_cp[q][smp] = make_float2((float)tc, (float)dl);
-      }
-    }
-  }
-  __syncthreads();
-  const int stride = gridDim.x * WPB;
-  for (int row = r0 + blockIdx.x * WPB + wave; row < a.Tf; row += stride) {
-    const double ti = a.t[row];
-    const int sg = a.seg[row];
-    double xbm = 0.0, xba = 0.0;
-    if (lane < a.K) {
-      const double xv = a.XT[(size_t)lane * a.Tp + row];
-      xbm = xv * ps.bm[lane];
-      xba = xv * ps.ba[lane];
-    }
-    xbm = wave_sum(xbm);
-    xba = wave_sum(xba);
-    const double trs = pred_trend(a, ps, series, row, ti, sg);
-    const double trend = trs * ysc;
-    const double addt = xba * ysc;
-    const double yhat = trend * (1.0 + xbm) + addt;
-    float ylo, yhi, tlo = (float)trend, thi = (float)trend;
-    const bool logi = a.growth == PF_GROWTH_LOGISTIC;
-    const double capr = logi ? a.cap[(size_t)series * a.Tp + row] : 0.0;
-    float z[PF_NQ];
-#pragma unroll
-    for (int c = 0; c < PF_NQ / 4; ++c) {
-      const pf_u4 rr = philox4x32_10(pf_u4{(uint32_t)c, (uint32_t)lane, (uint32_t)row, sid},
-                                     a.seed0, a.seed1);
-      pf_box_muller(pf_u01f(rr.x), pf_u01f(rr.y), z[4 * c + 0], z[4 * c + 1]);
-      pf_box_muller(pf_u01f(rr.z), pf_u01f(rr.w), z[4 * c + 2], z[4 * c + 3]);
-    }
-    const float sd = (float)(sigma * ysc);
-    const float u1 = (float)(1.0 + xbm);
-    const float addf = (float)addt;
-    float v[PF_NQ], tv[PF_NQ];
-    const bool random = pred_row_random(a, ti, t_max);
-    if (!random) {
-      const float base = (float)yhat;
-#pragma unroll
-      for (int q = 0; q < PF_NQ; ++q) {
-        const int smp = lane + 64 * q;
-        v[q] = (smp < a.N) ? fmaf(sd, z[q], base) : INFINITY;
-      }
-    } else {
-      const float tf = (float)ti, ysf = (float)ysc;
-#pragma unroll
-      for (int q = 0; q < PF_NQ; ++q) {
-        const int smp = lane + 64 * q;
-        if (smp < a.N) {
-          const int n = s_cnt[smp];
-          float trs_s;
-          if (!logi) {
-            float off = 0.0f;
-            if (n <= PF_MC_NCP) {
-              for (int c = 0; c < n; ++c) {
-                const float2 cp = s_cp[c][smp];
-                off = (tf >= cp.x) ? fmaf(cp.y, tf - cp.x, off) : off;
-              }
-            } else {
-              off = (float)mc_offset_slow(a.seed0, a.seed1, sid, smp, n, t_max, lam, ti);
-            }
-            trs_s = (float)trend + ysf * off;
-          } else if (n <= PF_MC_NCP && (n == 0 || tf < s_cp[0][smp].x)) {
-            trs_s = (float)trend;  // no new changepoint before t
-          } else if (n <= PF_MC_NCP) {
-            float kc = (float)ps.kseg[a.S], mc = (float)ps.mseg[a.S];
-            for (int c = 0; c < n; ++c) {
-              const float2 cp = s_cp[c][smp];
-              if (tf < cp.x) break;
-              const float kn = kc + cp.y;
-              mc = mc + (cp.x - mc) * (1.0f - kc / kn);
-              kc = kn;
-            }
-            trs_s = (float)(ysc * capr) / (1.0f + __expf(-(kc * (tf - mc))));
-          } else {
-            trs_s = (float)(ysc * capr * mc_logistic_slow(a.seed0, a.seed1, sid, smp, n, t_max, lam, ti,
-                                                          ps.kseg[a.S], ps.mseg[a.S]));
-          }
-          tv[q] = trs_s;
-          v[q] = fmaf(sd, z[q], fmaf(trs_s, u1, addf));
-        } else {
-          tv[q] = INFINITY;
-          v[q] = INFINITY;
-        }
-      }
-    }
-    float *buf = s_buf[wave];
-    float a0, a1;
-    wave_select_pair(v, a.k_lo, buf, a0, a1);
-    ylo = np_lerp(a0, a1, a.fr_lo);
-    float nv[PF_NQ];
-#pragma unroll
-    for (int q = 0; q < PF_NQ; ++q) nv[q] = (v[q] == INFINITY) ? INFINITY : -v[q];
-    wave_select_pair(nv, a.k_hi_neg, buf, a0, a1);
-    // a0 = -s[k_hi+1], a1 = -s[k_hi]
-    yhi = np_lerp(-a1, -a0, a.fr_hi);
-    if (random) {
-      wave_select_pair(tv, a.k_lo, buf, a0, a1);
-      tlo = np_lerp(a0, a1, a.fr_lo);
-#pragma unroll
-      for (int q = 0; q < PF_NQ; ++q) nv[q] = (tv[q] == INFINITY) ? INFINITY : -tv[q];
-      wave_select_pair(nv, a.k_hi_neg, buf, a0, a1);
-      thi = np_lerp(-a1, -a0, a.fr_hi);
-    }
-    if (lane == 0) {
-      const size_t o = (size_t)series * a.Tp + row;
-      a.ylo[o] = ylo;
-      a.yhi[o] = yhi;
-      if (a.tr) { a.trlo[o] = tlo; a.trhi[o] = thi; }
-    }
-  }
-}
+#include "pf_mc.h"
 
 // ============================================================================
 // C ABI
@@ -2366,16 +2089,12 @@ int pf_predict(pf_ctx *ctx, const pf_predict_args *p, void *stream) {
                   (k_predict_det<64>), grid, dim3(256), 0, (hipStream_t)stream, a);
   PF_HIP(ctx, hipGetLastError());
   if (a.N > 0) {
-    // sample mode: ~8 rows per wave; exact mode: the random rows (the
-    // horizon) spread over PF_MC_WAVES_PER_SERIES waves per series
-    int gx = (a.method == PF_INTERVAL_SAMPLE) ? (a.Tf + 8 * PF_MC_WPB - 1) / (8 * PF_MC_WPB)
-                                              : PF_MC_WAVES_PER_SERIES / PF_MC_WPB;
-    if (gx > (a.Tf + PF_MC_WPB - 1) / PF_MC_WPB) gx = (a.Tf + PF_MC_WPB - 1) / PF_MC_WPB;
-    if (gx < 1) gx = 1;
+    // exact mode: one block (PF_MC_WAVES waves) per series over the random
+    // rows (the horizon); sample mode: every row, <= 64 rows per wave
+    const int gx = (a.method == PF_INTERVAL_SAMPLE) ? (a.Tf + 64 * PF_MC_WAVES - 1) / (64 * PF_MC_WAVES) : 1;
     const dim3 gmc(gx, a.n_series);
     PF_TIMED_LAUNCH(ctx, "k_predict_mc", gmc.x * gmc.y, (hipStream_t)stream,
-                    (k_predict_mc<64, PF_MC_WPB>), gmc, dim3(PF_MC_WPB * 64), 0,
-                    (hipStream_t)stream, a);
+                    (k_predict_mc<64>), gmc, dim3(PF_MC_WAVES * 64), 0, (hipStream_t)stream, a);
     PF_HIP(ctx, hipGetLastError());
   }
   return 0;

@@ -1,0 +1,461 @@
+// pf_mc.h — K5: Monte-Carlo forecast rows.
+//
+// UPSTREAM predict_uncertainty → sample_posterior_predictive →
+// sample_predictive_trend (Prophet 0.7.1 / 1.0): per
+// sample, n ~ Poisson(S (T - 1)) new changepoints at t_c ~ U(1, T] with
+// delta ~ Laplace(0, lambda = mean|delta| + 1e-8); the trend is the fitted
+// piecewise trend continued over the concatenated changepoints; yhat sample
+// = trend_s (1 + Xb_m) + Xb_a + N(0, sigma_obs) y_scale; the interval ends are
+// np.nanpercentile(·, 2.5 / 97.5) with linear interpolation.
+//
+// Layout: one block of PF_MC_WAVES waves per (series, row range); a wave walks
+// a contiguous run of rows in time order; 16 samples per lane (sample
+// lane + 64 q).
+//   * Setup (block): every sample's changepoints are drawn once from its
+//     counter-based stream and packed into LDS in time order (prefix offsets;
+//     ~1.2 per sample at T = 1826).
+//   * Rows: a sample's trend is piecewise in t, so each lane keeps per-sample
+//     running state (linear: A = sum delta, B = sum delta tau_c, trend offset
+//     A tau - B with tau = t - 1; logistic: the logistic_gamma walk (k, m))
+//     and absorbs a changepoint only when t passes it — O(1) per sample-row.
+//   * The row's deterministic part (Xb, point trend) is computed lane-per-row
+//     for 64 rows at once and broadcast by readlane.
+//   * Selection: exact order statistics of up to four key sets (yhat lower /
+//     upper tail, trend lower / upper tail) with interleaved wave sorts
+//     (wave_tail_select).
+#pragma once
+
+#define PF_MC_WAVES 4        // waves per block
+#define PF_MC_CPCAP 4096     // packed changepoint slots per block (E = N S (T-1): 1.2k at T = 1826, 3.1k at 730)
+#define PF_MC_ABS (1u << 26)  // per-sample state: a changepoint was absorbed
+
+// ---- NS independent ascending wave sorts, interleaved step by step (ILP)
+template <int J, int NS>
+__device__ __forceinline__ void bitonic_step_n(float (&x)[NS], bool up) {
+  const bool tmin = ((pf_lane() & J) == 0) == up;
+  float p[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) p[s] = shfl_xor_f32<J>(x[s]);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) x[s] = tmin ? fminf(x[s], p[s]) : fmaxf(x[s], p[s]);
+}
+template <int K, int NS>
+__device__ __forceinline__ void bitonic_merge_n(float (&x)[NS]) {
+  const bool up = (pf_lane() & K) == 0 || K == 64;
+  if constexpr (K >= 64) bitonic_step_n<32>(x, up);
+  if constexpr (K >= 32) bitonic_step_n<16>(x, up);
+  if constexpr (K >= 16) bitonic_step_n<8>(x, up);
+  if constexpr (K >= 8) bitonic_step_n<4>(x, up);
+  if constexpr (K >= 4) bitonic_step_n<2>(x, up);
+  bitonic_step_n<1>(x, up);
+}
+template <int NS>
+__device__ __forceinline__ void wave_sort_asc_n(float (&x)[NS]) {
+  bitonic_merge_n<2>(x);
+  bitonic_merge_n<4>(x);
+  bitonic_merge_n<8>(x);
+  bitonic_merge_n<16>(x);
+  bitonic_merge_n<32>(x);
+  bitonic_merge_n<64>(x);
+}
+
+// Ranks kk[s] and kk[s] + 1 (0-indexed, ascending) of NS key sets held 16 per
+// lane: set s reads src[s >> 1 ? 1 : 0] (yhat / trend samples), negated for
+// odd s (upper tail); absent samples are NaN (ignored by fminf/fmaxf, never
+// below a threshold).  Threshold U_s = the (kk+2)-th smallest lane minimum, so
+// at least kk+2 keys are <= U_s; the keys strictly below U_s (M_s of them) are
+// compacted into LDS and sorted, and every rank >= M_s equals U_s (exact under
+// ties — trend samples without a new changepoint all equal the point trend).
+// Falls back to a bisection on the ordered bit patterns when kk + 2 > 64 or
+// more than 64 keys fall below U_s.  buf: NS * 64 floats of wave-private LDS.
+template <int NS>
+__device__ __forceinline__ void wave_tail_select(const float (&v)[PF_NQ], const float (&tv)[PF_NQ],
+                                                 const int (&kk)[NS], float *buf, float (&o0)[NS],
+                                                 float (&o1)[NS]) {
+  const int lane = pf_lane();
+  auto src = [&](int s, int q) -> float { return (s < 2) ? v[q] : tv[q]; };
+  float lm[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    if (s & 1) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int q = 0; q < PF_NQ; ++q) mx = fmaxf(mx, src(s, q));
+      lm[s] = -mx;
+    } else {
+      float mn = INFINITY;
+#pragma unroll
+      for (int q = 0; q < PF_NQ; ++q) mn = fminf(mn, src(s, q));
+      lm[s] = mn;
+    }
+  }
+  wave_sort_asc_n(lm);
+  float U[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) U[s] = (kk[s] + 1 < 64) ? readlane_f32(lm[s], kk[s] + 1) : INFINITY;
+  int M[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) M[s] = 0;
+#pragma unroll
+  for (int q = 0; q < PF_NQ; ++q) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const float x = src(s, q);
+      const bool pr = (s & 1) ? (x > -U[s]) : (x < U[s]);
+      const unsigned long long m = __ballot(pr);
+      const int pos = M[s] + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (pr && pos < 64) buf[s * 64 + pos] = (s & 1) ? -x : x;
+      M[s] += __popcll(m);
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  float c[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) c[s] = (lane < M[s]) ? buf[s * 64 + lane] : INFINITY;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  wave_sort_asc_n(c);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int k = kk[s];
+    if (k + 1 < 64 && M[s] <= 64) {
+      o0[s] = (k < M[s]) ? readlane_f32(c[s], k) : U[s];
+      o1[s] = (k + 1 < M[s]) ? readlane_f32(c[s], k + 1) : U[s];
+    } else {
+      for (int want = 0; want < 2; ++want) {
+        uint32_t lo = 0u, hi = 0xFFFFFFFFu;
+        while (lo < hi) {
+          const uint32_t mid = lo + ((hi - lo) >> 1);
+          int cnt = 0;
+#pragma unroll
+          for (int q = 0; q < PF_NQ; ++q) {
+            const float x = src(s, q);
+            const float kx = (x != x) ? INFINITY : ((s & 1) ? -x : x);
+            cnt += __popcll(__ballot(pf_f2ord(kx) <= mid));
+          }
+          if (cnt >= k + want + 1) hi = mid; else lo = mid + 1;
+        }
+        if (want == 0) o0[s] = pf_ord2f(lo); else o1[s] = pf_ord2f(lo);
+      }
+    }
+  }
+}
+
+// sample smp's c-th new changepoint: tau = t_c - 1 ~ U(0, T - 1], delta ~ Laplace(0, lam)
+__device__ __forceinline__ void mc_sample_cp(uint32_t seed0, uint32_t seed1, uint32_t series, int smp,
+                                             int c, double t_max, double lam, double &tau, double &dl) {
+  const pf_u4 rc = philox4x32_10(pf_u4{(uint32_t)smp, (uint32_t)(c + 1), (uint32_t)series, 0x7EE2D00Du},
+                                 seed0 ^ 0x5A5A5A5Au, seed1);
+  tau = pf_u01d(rc.x, rc.y) * (t_max - 1.0);
+  const double ul = pf_u01d(rc.z, rc.w);
+  dl = (ul >= 0.5) ? -lam * log(2.0 - ul - ul) : lam * log(ul + ul);
+}
+
+// Poisson(lam_pois) count of sample smp by inversion (e_neg = exp(-lam_pois))
+__device__ __forceinline__ int mc_sample_count(uint32_t seed0, uint32_t seed1, uint32_t series, int smp,
+                                               double lam_pois, double e_neg) {
+  const pf_u4 r0 = philox4x32_10(pf_u4{(uint32_t)smp, 0u, (uint32_t)series, 0x7EE2D00Du},
+                                 seed0 ^ 0x5A5A5A5Au, seed1);
+  const double u0 = pf_u01d(r0.x, r0.y);
+  int n = 0;
+  if (lam_pois > 0.0) {
+    double p = e_neg, F = p;
+    while (u0 > F && n < 100000) {
+      ++n;
+      p *= lam_pois / (double)n;
+      F += p;
+      if (p == 0.0 && F < u0) break;
+    }
+  }
+  return n;
+}
+
+// Trend sample at tau re-derived from the counter-based stream (blocks whose
+// changepoints overflow the LDS slots: horizons far beyond the history).
+__device__ __forceinline__ float mc_trend_direct(uint32_t seed0, uint32_t seed1, uint32_t series, int smp, int n,
+                                                 double t_max, double lam, double tau, bool logi, double trend,
+                                                 double ysc, double capy, double k0, double m0) {
+  if (!logi) {
+    double off = 0.0;
+    for (int c = 0; c < n; ++c) {
+      double tc, dl;
+      mc_sample_cp(seed0, seed1, series, smp, c, t_max, lam, tc, dl);
+      if (tau >= tc) off += dl * (tau - tc);
+    }
+    return (float)(trend + ysc * off);
+  }
+  // logistic: absorb the changepoints before tau in time order (selection by
+  // repeated minimum; no per-sample storage)
+  double kc = k0, mc = m0, last = -1.0;
+  bool any = false;
+  for (int it = 0; it < n; ++it) {
+    double best = INFINITY, bdl = 0.0;
+    for (int c = 0; c < n; ++c) {
+      double tc, dl;
+      mc_sample_cp(seed0, seed1, series, smp, c, t_max, lam, tc, dl);
+      if (tc > last && tc < best) { best = tc; bdl = dl; }
+    }
+    if (!(best <= tau)) break;
+    const double kn = kc + bdl;
+    mc = mc + (1.0 + best - mc) * (1.0 - kc / kn);
+    kc = kn;
+    last = best;
+    any = true;
+  }
+  if (!any) return (float)trend;
+  return (float)(capy / (1.0 + exp(-(kc * (1.0 + tau - mc)))));
+}
+
+// The wave's rows [row_b, row_e).  DIRECT: every trend sample re-derived from
+// the stream (s_meta = count); otherwise the per-sample running state over
+// the packed changepoints.
+template <bool DIRECT>
+__device__ __forceinline__ void mc_rows(const PredKArgs &a, const PredSeries &ps, const float2 *s_cp,
+                                        const uint32_t *s_meta, float *buf, int series, uint32_t sid,
+                                        double t_max, int row_b, int row_e) {
+  const int lane = pf_lane();
+  const int N = a.N;
+  const bool logi = a.growth == PF_GROWTH_LOGISTIC;
+  const double ysc = ps.ysc, lam = ps.lam;
+  const float sd = (float)(ps.sigma * ysc);
+  const double k0 = ps.kseg[a.S], m0 = ps.mseg[a.S];
+  // per-sample trend state: st = index of the next changepoint (its tau /
+  // delta held in nxt / nxd) | end << 13 | PF_MC_ABS once one was absorbed
+  uint32_t st[PF_NQ];
+  float nxt[PF_NQ], nxd[PF_NQ], s1[PF_NQ], s2[PF_NQ];
+  if constexpr (!DIRECT) {
+#pragma unroll
+    for (int q = 0; q < PF_NQ; ++q) {
+      const int smp = lane + 64 * q;
+      const uint32_t meta = (smp < N) ? s_meta[smp] : 0u;
+      const uint32_t p0 = meta & 0x1FFFu, e0 = (meta >> 13) & 0x1FFFu;
+      st[q] = meta;
+      const float2 cp0 = (p0 < e0) ? s_cp[p0] : make_float2(INFINITY, 0.0f);
+      nxt[q] = cp0.x;
+      nxd[q] = cp0.y;
+      s1[q] = logi ? (float)k0 : 0.0f;
+      s2[q] = logi ? (float)m0 : 0.0f;
+    }
+  }
+  const int kk4[4] = {a.k_lo, a.k_hi_neg, a.k_lo, a.k_hi_neg};
+  const int kk2[2] = {a.k_lo, a.k_hi_neg};
+  for (int c0 = row_b; c0 < row_e; c0 += 64) {
+    const int nr = min(64, row_e - c0);
+    // lane-per-row deterministic part (same arithmetic as k_predict_det)
+    const int myrow = c0 + lane;
+    const bool rv = lane < nr;
+    double ti = 0.0, xbm = 0.0, xba = 0.0, trs = 0.0, capr = 0.0;
+    if (rv) {
+      ti = a.t[myrow];
+      const int sg = a.seg[myrow];
+      for (int f = 0; f < a.K; ++f) {
+        const double xv = a.XT[(size_t)f * a.Tp + myrow];
+        xbm += xv * ps.bm[f];
+        xba += xv * ps.ba[f];
+      }
+      trs = pred_trend(a, ps, series, myrow, ti, sg);
+      if (logi) capr = a.cap[(size_t)series * a.Tp + myrow];
+    }
+    const double l_trend = trs * ysc, l_add = xba * ysc;
+    const float lf_tau = (float)(ti - 1.0), lf_trend = (float)l_trend, lf_u1 = (float)(1.0 + xbm);
+    const float lf_add = (float)l_add, lf_yhat = (float)(l_trend * (1.0 + xbm) + l_add);
+    const float lf_capy = (float)(ysc * capr);
+    const int l_rand = (rv && pred_row_random(a, ti, t_max)) ? 1 : 0;
+    float o_ylo = 0.f, o_yhi = 0.f, o_tlo = 0.f, o_thi = 0.f;
+    PF_STAMP1(2);
+    for (int r = 0; r < nr; ++r) {
+      PF_STAMP1(3);
+      if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) PF_COUNT(9);
+      const int row = c0 + r;
+      const float tau = readlane_f32(lf_tau, r);
+      const float trendf = readlane_f32(lf_trend, r);
+      const float u1 = readlane_f32(lf_u1, r), addf = readlane_f32(lf_add, r);
+      const bool random = __builtin_amdgcn_readlane(l_rand, r) != 0;
+      const float yh = readlane_f32(lf_yhat, r);
+      float v[PF_NQ], tv[PF_NQ];
+      float ylo, yhi, tlo = trendf, thi = trendf;
+      if (random) {
+        const float capy = readlane_f32(lf_capy, r);
+        if constexpr (DIRECT) {
+#pragma unroll
+          for (int q = 0; q < PF_NQ; ++q) {
+            const int smp = lane + 64 * q;
+            tv[q] = (smp < N) ? mc_trend_direct(a.seed0, a.seed1, sid, smp, (int)s_meta[smp], t_max, lam,
+                                                (double)tau, logi, (double)trendf, ysc, (double)capy, k0, m0)
+                              : __builtin_nanf("");
+          }
+        } else {
+          // absorb the changepoints passed since the previous row: one pass
+          // over the samples with the next changepoint held in registers (the
+          // LDS loads of different samples overlap), repeated only if a sample
+          // passed two changepoints since the previous row
+          while (true) {
+#pragma unroll
+            for (int q = 0; q < PF_NQ; ++q) {
+              const bool cr = tau >= nxt[q];
+              if (__ballot(cr) != 0ull) {
+                if (cr) {
+                  const uint32_t p = (st[q] & 0x1FFFu) + 1u, e = (st[q] >> 13) & 0x1FFFu;
+                  if (!logi) {
+                    s1[q] += nxd[q];
+                    s2[q] = fmaf(nxd[q], nxt[q], s2[q]);
+                  } else {
+                    const float kn = s1[q] + nxd[q];
+                    s2[q] = s2[q] + (1.0f + nxt[q] - s2[q]) * (1.0f - s1[q] / kn);
+                    s1[q] = kn;
+                  }
+                  st[q] = (st[q] & ~0x1FFFu) | p | PF_MC_ABS;
+                  const float2 cp = (p < e) ? s_cp[p] : make_float2(INFINITY, 0.0f);
+                  nxt[q] = cp.x;
+                  nxd[q] = cp.y;
+                }
+              }
+            }
+            unsigned long long more = 0ull;
+#pragma unroll
+            for (int q = 0; q < PF_NQ; ++q) more |= __ballot(tau >= nxt[q]);
+            if (more == 0ull) break;
+          }
+          PF_STAMP1(4);
+          const float ysf = (float)ysc;
+#pragma unroll
+          for (int q = 0; q < PF_NQ; ++q) {
+            float trs_s;
+            if (!logi) trs_s = fmaf(ysf, fmaf(s1[q], tau, -s2[q]), trendf);
+            else trs_s = (st[q] & PF_MC_ABS) ? capy / (1.0f + __expf(-(s1[q] * (1.0f + tau - s2[q])))) : trendf;
+            tv[q] = (lane + 64 * q < N) ? trs_s : __builtin_nanf("");
+          }
+        }
+      }
+      PF_STAMP1(5);
+#pragma unroll
+      for (int c = 0; c < PF_NQ / 4; ++c) {
+        const pf_u4 rr = philox4x32_10(pf_u4{(uint32_t)c, (uint32_t)lane, (uint32_t)row, sid},
+                                       a.seed0, a.seed1);
+        float z[4];
+        pf_box_muller(pf_u01f(rr.x), pf_u01f(rr.y), z[0], z[1]);
+        pf_box_muller(pf_u01f(rr.z), pf_u01f(rr.w), z[2], z[3]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int q = 4 * c + j;
+          v[q] = random ? fmaf(sd, z[j], fmaf(tv[q], u1, addf)) : fmaf(sd, z[j], yh);
+          if (lane + 64 * q >= N) v[q] = __builtin_nanf("");
+        }
+      }
+      PF_STAMP1(6);
+      if (random) {
+        float o0[4], o1[4];
+        wave_tail_select<4>(v, tv, kk4, buf, o0, o1);
+        if (N == 1) { for (int s = 0; s < 4; ++s) o1[s] = o0[s]; }
+        ylo = np_lerp(o0[0], o1[0], a.fr_lo);
+        yhi = np_lerp(-o1[1], -o0[1], a.fr_hi);
+        tlo = np_lerp(o0[2], o1[2], a.fr_lo);
+        thi = np_lerp(-o1[3], -o0[3], a.fr_hi);
+      } else {
+        float o0[2], o1[2];
+        wave_tail_select<2>(v, v, kk2, buf, o0, o1);
+        if (N == 1) { o1[0] = o0[0]; o1[1] = o0[1]; }
+        ylo = np_lerp(o0[0], o1[0], a.fr_lo);
+        yhi = np_lerp(-o1[1], -o0[1], a.fr_hi);
+      }
+      PF_STAMP1(7);
+      if (lane == r) { o_ylo = ylo; o_yhi = yhi; o_tlo = tlo; o_thi = thi; }
+    }
+    if (rv) {
+      const size_t o = (size_t)series * a.Tp + myrow;
+      a.ylo[o] = o_ylo;
+      a.yhi[o] = o_yhi;
+      if (a.tr) { a.trlo[o] = o_tlo; a.trhi[o] = o_thi; }
+    }
+  }
+}
+
+template <int KMAX>
+__global__ __launch_bounds__(PF_MC_WAVES * 64) void k_predict_mc(PredKArgs a) {
+  constexpr int NT = PF_MC_WAVES * 64;
+  constexpr int SPT = (64 * PF_NQ) / NT;  // samples per thread in the setup
+  __shared__ PredSeries ps;
+  __shared__ float2 s_cp[PF_MC_CPCAP];     // (tau_c, delta), each sample's run in time order
+  __shared__ uint32_t s_meta[64 * PF_NQ];  // first slot | end << 13  (overflow: count)
+  __shared__ float s_buf[PF_MC_WAVES][4 * 64];
+  __shared__ double s_wsum[PF_MC_WAVES];
+  __shared__ int s_r0;
+  const int series = blockIdx.y, lane = pf_lane(), wave = pf_wave(), tid = threadIdx.x;
+  const uint32_t sid = a.series_id ? a.series_id[series] : (uint32_t)series;
+  const int N = a.N;
+  PF_STAMP1(0);
+  if (tid == 0) s_r0 = (a.method == PF_INTERVAL_SAMPLE) ? 0 : a.Tf;
+  pred_setup(a, series, ps);
+  const double t_max = a.t[a.Tf - 1];
+  __syncthreads();
+  if (a.method != PF_INTERVAL_SAMPLE) {
+    // first random-trend row (rows sorted by t): independent loads, min
+    int loc = a.Tf;
+    for (int b0 = 0; b0 < a.Tf; b0 += 8 * NT) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int r = b0 + i * NT + tid;
+        if (r < a.Tf && pred_row_random(a, a.t[r], t_max)) loc = min(loc, r);
+      }
+    }
+    if (loc < a.Tf) atomicMin(&s_r0, loc);
+  }
+  // ---- per-sample new changepoints, packed in time order
+  const double lam = ps.lam;
+  const bool any_random = pred_row_random(a, t_max, t_max);
+  const double lam_pois = any_random ? (double)a.S * (t_max - 1.0) : 0.0;
+  int cnt[SPT];
+  int tot = 0;
+  {
+    const double e_neg = exp(-lam_pois);
+#pragma unroll
+    for (int i = 0; i < SPT; ++i) {
+      const int smp = tid + i * NT;
+      cnt[i] = (any_random && smp < N) ? mc_sample_count(a.seed0, a.seed1, sid, smp, lam_pois, e_neg) : 0;
+      tot += cnt[i];
+    }
+  }
+  const double inc = wave_prefix_sum((double)tot);
+  if (lane == 63) s_wsum[wave] = inc;
+  __syncthreads();
+  double total = 0.0, base = inc - (double)tot;
+  for (int w = 0; w < PF_MC_WAVES; ++w) {
+    total += s_wsum[w];
+    if (w < wave) base += s_wsum[w];
+  }
+  const bool ovf = total > (double)PF_MC_CPCAP;  // uniform
+  int off = (int)base;
+#pragma unroll
+  for (int i = 0; i < SPT; ++i) {
+    const int smp = tid + i * NT;
+    const int n = cnt[i];
+    if (!ovf) {
+      for (int c = 0; c < n; ++c) {
+        double tau, dl;
+        mc_sample_cp(a.seed0, a.seed1, sid, smp, c, t_max, lam, tau, dl);
+        const float tf = (float)tau;
+        int q = c;
+        while (q > 0 && s_cp[off + q - 1].x > tf) { s_cp[off + q] = s_cp[off + q - 1]; --q; }
+        s_cp[off + q] = make_float2(tf, (float)dl);
+      }
+      s_meta[smp] = (uint32_t)off | ((uint32_t)(off + n) << 13);
+    } else {
+      s_meta[smp] = (uint32_t)n;
+    }
+    off += n;
+  }
+  __syncthreads();
+  PF_STAMP1(1);
+  const int r0 = s_r0;
+  const int nrows = a.Tf - r0;
+  if (nrows <= 0) return;
+  const int nw = gridDim.x * PF_MC_WAVES;
+  const int rpw = (nrows + nw - 1) / nw;
+  const int row_b = r0 + (blockIdx.x * PF_MC_WAVES + wave) * rpw;
+  const int row_e = min(row_b + rpw, a.Tf);
+  if (row_b >= row_e) return;  // no block-level sync below
+  if (ovf) mc_rows<true>(a, ps, s_cp, s_meta, s_buf[wave], series, sid, t_max, row_b, row_e);
+  else mc_rows<false>(a, ps, s_cp, s_meta, s_buf[wave], series, sid, t_max, row_b, row_e);
+}

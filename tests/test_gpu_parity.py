@@ -443,3 +443,35 @@ def test_timing_records(eng):
     for k in ("k_prepare", "k_fit", "k_polish", "k_predict_det", "k_predict_mc"):
         assert k in names
     assert all(r[1] > 0 for r in rec)
+
+
+@pytest.mark.parametrize("horizon", [90, 365])
+def test_future_intervals_vs_oracle_sampler(eng, horizon):
+    """730-day history (configs[3] shape).  90 days: ~3.1k new changepoints
+    per series fit the kernel's packed LDS slots; 365 days (~12.5k) overflow
+    them and the block re-derives every trend sample from its counter-based
+    stream.  Both against the oracle's literal per-sample loop (UPSTREAM
+    sample_predictive_trend), same theta: interval widths agree within MC
+    error along the horizon."""
+    ds = synthetic.daily_dates("2016-01-01", "2017-12-30")
+    Y = synthetic.sales_matrix(4, ds, config_index=3)
+    g = _grid(eng, ds)
+    fit = eng.fit(g, _Y(g, Y))
+    fut = B.future_dates(ds, horizon)
+    fg = eng.predict_grid(fit, fut)
+    out = eng.predict(fit, fg, seed=21)
+    th = fit.theta.cpu().numpy()
+    T = len(ds)
+    for s in range(4):
+        setup = po.build_problem(ds, Y[s])
+        par = po.params_from_theta(th[s], setup.problem.S)
+        o = po.sample_uncertainty(setup, par, fut, n_samples=1000, rng=np.random.default_rng(100 + s))
+        for r in (T + horizon // 3, T + horizon - 1):
+            for lo, hi, tol in (("yhat_lower", "yhat_upper", 0.25), ("trend_lower", "trend_upper", 0.4)):
+                w_o = o[hi][r] - o[lo][r]
+                w_g = float(out[hi][s, r] - out[lo][s, r])
+                # (a series whose deltas are all ~0 has lambda ~ 1e-8: no band)
+                assert abs(w_g - w_o) < tol * w_o + 1e-5 * setup.hist.y_scale, (s, r, lo, w_g, w_o)
+        yh = out["yhat"][s, :fg.T].cpu().numpy()
+        assert np.all(out["yhat_lower"][s, :fg.T].cpu().numpy() <= yh + 1e-3 * abs(yh).max())
+        assert np.all(out["yhat_upper"][s, :fg.T].cpu().numpy() >= yh - 1e-3 * abs(yh).max())
