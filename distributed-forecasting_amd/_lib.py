@@ -22,6 +22,7 @@ PF_ST_CONSTANT = 50
 EXPORTED = ["pf_ctx_create", "pf_ctx_destroy", "pf_last_error", "pf_default_fit_opts",
             "pf_num_changepoints", "pf_build_grid", "pf_prepare", "pf_objective_grad",
             "pf_fit", "pf_predict", "pf_set_timing", "pf_read_timings", "pf_cv_metrics"]
+PF_MAX_COMP = 32  # include/prophet_hip.h
 PF_INTERVAL = {"exact": 0, "sample": 1}
 CV_METRICS = ["mse", "rmse", "mae", "mape", "smape", "coverage"]
 
@@ -55,7 +56,7 @@ class PfFitOpts(ctypes.Structure):
                 ("tol_rel_obj", ctypes.c_double), ("tol_grad", ctypes.c_double),
                 ("tol_rel_grad", ctypes.c_double), ("tol_param", ctypes.c_double),
                 ("max_iter", i32), ("history", i32), ("polish", i32), ("polish_max_iter", i32),
-                ("lbfgs_warmup", i32), ("_pad", i32)]
+                ("lbfgs_warmup", i32), ("lbfgs_warmup_evals", i32)]
 
 
 class PfPredictArgs(ctypes.Structure):
@@ -66,7 +67,7 @@ class PfPredictArgs(ctypes.Structure):
                 ("yhat", vp), ("yhat_lower", vp), ("yhat_upper", vp),
                 ("trend", vp), ("trend_lower", vp), ("trend_upper", vp),
                 ("mult_terms", vp), ("add_terms", vp),
-                ("n_comp", i32), ("comp_col0", i32 * 4), ("comp_ncol", i32 * 4), ("comp", vp),
+                ("n_comp", i32), ("comp_col0", i32 * PF_MAX_COMP), ("comp_ncol", i32 * PF_MAX_COMP), ("comp", vp),
                 ("series_id", vp)]
 
 

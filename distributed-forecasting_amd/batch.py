@@ -147,6 +147,7 @@ class GridSpec:
     start_ns: int
     t_scale_ns: int
     t_change: torch.Tensor
+    holidays: object = None     # HolidaySpec of the fit grid (None: no holiday columns)
 
 
 def _dense(A, n: int, T: int, T_pad: int, dev) -> torch.Tensor:
@@ -180,11 +181,13 @@ class FittedBatch:
 
     @classmethod
     def fit_dense(cls, engine: E.Engine, fit_ds: np.ndarray, Y, history_dates=None,
-                  series_ids=None, polish: bool = True, seasons=None, cap=None) -> "FittedBatch":
+                  series_ids=None, polish: bool = True, seasons=None, cap=None,
+                  holidays=None) -> "FittedBatch":
         """Fit every row of Y ([n, T] numpy or device tensor, raw y) on the
         sorted date grid ``fit_ds`` (K1 grid + K2/K3 fit).  ``seasons``
         overrides the auto rules (CV folds reuse the parent's seasonalities,
-        UPSTREAM diagnostics.prophet_copy)."""
+        UPSTREAM diagnostics.prophet_copy); ``holidays`` (holidays.HolidaySpec)
+        appends its indicator columns."""
         cfg = engine.config
         fit_ds = np.asarray(fit_ds, np.int64)
         T = fit_ds.shape[0]
@@ -197,7 +200,8 @@ class FittedBatch:
             seasons = cfg.seasons(start, int(fit_ds[-1]), min_positive_diff(fit_ds))
         grid = E.build_grid(fit_ds, seasons, start_ns=start, t_scale_ns=t_scale,
                             n_changepoints=cfg.n_changepoints,
-                            changepoint_range=cfg.changepoint_range, device=engine.device)
+                            changepoint_range=cfg.changepoint_range, device=engine.device,
+                            holidays=holidays)
         dev = torch.device("cuda", engine.device)
         n = int(Y.shape[0])
         Yd = torch.zeros((n, grid.T_pad), dtype=torch.float64, device=dev)
@@ -216,7 +220,7 @@ class FittedBatch:
 
     def spec(self) -> GridSpec:
         g = self.fit.grid
-        return GridSpec(list(g.seasons), int(g.start_ns), int(g.t_scale_ns), g.t_change)
+        return GridSpec(list(g.seasons), int(g.start_ns), int(g.t_scale_ns), g.t_change, g.holidays)
 
     def predict(self, ds_ns: np.ndarray, *, seed: int = 0, n_samples: int | None = None,
                 components: bool = True, cap=None):

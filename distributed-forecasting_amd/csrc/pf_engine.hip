@@ -304,6 +304,27 @@ enum { MODE_MULT = 0, MODE_ADD = 1, MODE_MIXED = 2 };
 // bit 2 of the MODE template argument selects the logistic-growth variant
 // (compiled separately so the linear kernels carry none of its registers)
 #define PF_MODE_LOGI 4
+// bit 3: wide variant, P up to 128 — two parameter words per lane, parameter
+// p = lane + 64 h in word h (word 1 holds only beta's: 3 + S <= 64)
+#define PF_MODE_WIDE 8
+template <int MODE>
+struct ModeTr {
+  static constexpr int PW = (MODE & PF_MODE_WIDE) ? 2 : 1;
+};
+// this lane's parameter words
+template <int PW>
+struct PV {
+  double v[PW];
+  __device__ __forceinline__ double &operator[](int i) { return v[i]; }
+  __device__ __forceinline__ double operator[](int i) const { return v[i]; }
+};
+template <int PW>
+__device__ __forceinline__ PV<PW> pv_zero() {
+  PV<PW> r;
+#pragma unroll
+  for (int h = 0; h < PW; ++h) r[h] = 0.0;
+  return r;
+}
 
 struct FitKArgs {
   int T, Tp, K, S, growth, P, NB;
@@ -431,7 +452,7 @@ __device__ __forceinline__ void row_features(const double *__restrict__ XT, int 
   for (int f = KF; f < KMAX; ++f) x[f] = (f < K) ? XT[(size_t)f * Tp + i] : 0.0;
 }
 
-static constexpr size_t kLbBytes = 9 * 1024;
+template <int PW>
 struct LbLds;
 // LDS layout of the fit kernels.  Fixed part + a union region U that holds
 // the L-BFGS state during the Stan phase (k_fit) and {Hessian tile
@@ -441,7 +462,7 @@ struct FitSmem {
   static constexpr int NSET = ((MODE & 3) == 2) ? 2 : 1;  // (mult, add) gradient sets
   static constexpr int NL = NW * 64;                 // row-pass threads
   double *y;        // [ny] lane-blocked y_scaled (position r*NL + L)
-  double *th;       // [64]
+  double *th;       // [128]
   double *kseg;     // [64]
   double *mseg;     // [64]
   double *bm, *ba;  // [KMAX]
@@ -449,7 +470,7 @@ struct FitSmem {
   double *wt0, *wt1;      // [NW] per-wave totals of G, G*t
   double *cpre0, *cpre1;  // [64] per changepoint: owner thread's sum before its first row
   double *rrw;      // [NW]
-  double *gout;     // [64]
+  double *gout;     // [128]
   double *fout;     // [4]
   double *sig;      // [2] sigma, 1/sigma^2 of the published point
   double *gpart;    // [NW][NSET*KMAX] per-wave beta-gradient totals
@@ -459,18 +480,19 @@ struct FitSmem {
   int *flag;        // [4] loop control
   double *ctc, *csg, *csm, *csa;  // [64] t_change[j], sigmas[f], s_m[f], s_a[f] (0 past the end)
   double *U;        // union region
-  struct LbLds *lb; // U view (Stan phase)
+  LbLds<ModeTr<MODE>::PW> *lb; // U view (Stan phase)
   int LD;           // stride of H / M in U (polish)
   static __host__ __device__ size_t fixed_doubles(int ny) {
-    return (size_t)ny + 64 * 3 + 2 * KMAX + 2 * NL + 2 * NW + 128 + NW + 64 + 4 + 2 +
+    return (size_t)ny + 64 * 4 + 2 * KMAX + 2 * NL + 2 * NW + 128 + NW + 128 + 4 + 2 +
            (size_t)NW * NSET * KMAX + 128 + 32 + 32 + 4 + 4 * 64;
   }
   static __host__ __device__ size_t union_bytes(int P, bool polish) {
-    if (!polish) return kLbBytes;
+    const size_t lbb = sizeof(LbLds<ModeTr<MODE>::PW>) + 16;
+    if (!polish) return lbb;
     const size_t tiles = (size_t)10 * 4 * 64 * sizeof(double);
     const int LD = P | 1;
     const size_t hm = 2 * (size_t)P * LD * sizeof(double);
-    size_t u = kLbBytes > tiles ? kLbBytes : tiles;
+    size_t u = lbb > tiles ? lbb : tiles;
     return u > hm ? u : hm;
   }
   static __host__ __device__ size_t bytes(int ny, int P, bool polish) {
@@ -479,7 +501,7 @@ struct FitSmem {
   __device__ void carve(char *base, int ny, int P) {
     double *p = reinterpret_cast<double *>(base);
     y = p; p += ny;
-    th = p; p += 64;
+    th = p; p += 128;
     kseg = p; p += 64;
     mseg = p; p += 64;
     bm = p; p += KMAX;
@@ -491,7 +513,7 @@ struct FitSmem {
     cpre0 = p; p += 64;
     cpre1 = p; p += 64;
     rrw = p; p += NW;
-    gout = p; p += 64;
+    gout = p; p += 128;
     fout = p; p += 4;
     sig = p; p += 2;
     gpart = p; p += (size_t)NW * NSET * KMAX;
@@ -508,7 +530,7 @@ struct FitSmem {
     size_t off = (size_t)(reinterpret_cast<char *>(p) - base);
     off = (off + 15) & ~(size_t)15;
     U = reinterpret_cast<double *>(base + off);
-    lb = reinterpret_cast<struct LbLds *>(U);
+    lb = reinterpret_cast<LbLds<ModeTr<MODE>::PW> *>(U);
     LD = P | 1;
   }
 };
@@ -531,11 +553,16 @@ __device__ __forceinline__ double logistic_mseg(double kl, double tcl, double m,
 }
 
 template <int NW, int KMAX, int MODE>
-__device__ __forceinline__ void publish_theta(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, double x) {
+__device__ __forceinline__ void publish_theta(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm,
+                                              const PV<ModeTr<MODE>::PW> &xv) {
+  constexpr int PW = ModeTr<MODE>::PW;
   const int lane = pf_lane();
   if (pf_wave() != 0) return;
   const int P = a.P, S = a.S, K = a.K;
-  if (lane < P) sm.th[lane] = x;
+  const double x = xv[0];
+#pragma unroll
+  for (int h = 0; h < PW; ++h)
+    if (lane + 64 * h < P) sm.th[lane + 64 * h] = xv[h];
   const double k = readlane_f64(x, 0), m = readlane_f64(x, 1);
   // delta_j sits in lane 2+j
   const double dj = __shfl(x, (lane + 2) & 63, 64);
@@ -557,7 +584,11 @@ __device__ __forceinline__ void publish_theta(const FitKArgs &a, FitSmem<NW, KMA
     sm.kseg[lane] = kl;
     sm.mseg[lane] = m - (lane == 0 ? 0.0 : ctd_ex);
   }
-  const double bval = __shfl(x, (lane + 3 + S) & 63, 64);
+  double bval = __shfl(x, (lane + 3 + S) & 63, 64);
+  if constexpr (PW > 1) {
+    const double b1 = __shfl(xv[1], (lane + 3 + S) & 63, 64);
+    if (lane + 3 + S >= 64) bval = b1;
+  }
   if (lane < KMAX) {
     const double bv = (lane < K) ? bval : 0.0;
     sm.bm[lane] = bv * sm.csm[lane];
@@ -736,9 +767,13 @@ __device__ __forceinline__ void wave_sum2(double a, double b, double &ta, double
 // directional derivative; pass pdir = 0 if unused).  Returns true if f or g
 // is not finite (Stan ModelAdaptor error -> line-search retreat).
 template <int NW, int KMAX, int MODE>
-__device__ __forceinline__ bool eval_assemble(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, double x,
-                                              double pdir, double &f, double &g, double &gp) {
+__device__ __forceinline__ bool eval_assemble(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm,
+                                              const PV<ModeTr<MODE>::PW> &xv,
+                                              const PV<ModeTr<MODE>::PW> &pdir, double &f,
+                                              PV<ModeTr<MODE>::PW> &g, double &gp) {
+  constexpr int PW = ModeTr<MODE>::PW;
   const int lane = pf_lane();
+  const double x = xv[0];
   const int P = a.P, S = a.S, T = a.T;
   const bool linear = (a.growth == PF_GROWTH_LINEAR);
   double rrt = 0.0, tot0 = 0.0, tot1 = 0.0;
@@ -834,10 +869,10 @@ __device__ __forceinline__ bool eval_assemble(const FitKArgs &a, FitSmem<NW, KMA
   } else if (p == 2 + S) {
     gv = (double)T - inv_s2 * rrt + 4.0 * sigma * sigma;
     fterm = 2.0 * sigma * sigma + (double)T * ls;
-  } else if (p < P) {
+  }
+  // beta f2 (parameter 3 + S + f2): Xb prior + the per-wave partials
+  auto beta_term = [&](int f2, double bv, double &gb, double &fb) {
     constexpr int NS = ((MODE & 3) == MODE_MIXED) ? 2 : 1;
-    const int f2 = p - 3 - S;
-    const double bv = x;
     const double sgm = sm.csg[f2];
     double gm = 0.0, ga = 0.0;
 #pragma unroll
@@ -850,15 +885,26 @@ __device__ __forceinline__ bool eval_assemble(const FitKArgs &a, FitSmem<NW, KMA
     double gl = 0.0;
     if ((MODE & 3) != MODE_ADD) gl += sm.csm[f2] * gm;
     if ((MODE & 3) != MODE_MULT) gl += sm.csa[f2] * ga;
-    gv = -inv_s2 * gl + bv / (sgm * sgm);
-    fterm = bv * bv / (2.0 * sgm * sgm);
+    gb = -inv_s2 * gl + bv / (sgm * sgm);
+    fb = bv * bv / (2.0 * sgm * sgm);
+  };
+  if (p > 2 + S && p < P) beta_term(p - 3 - S, x, gv, fterm);
+  g[0] = (p < P) ? gv : 0.0;
+  bool bad = (p < P && !isfinite(gv));
+  double gpl = g[0] * pdir[0];
+  if constexpr (PW > 1) {
+    const int p1 = lane + 64;
+    double g1 = 0.0, f1 = 0.0;
+    if (p1 < P) beta_term(p1 - 3 - S, xv[1], g1, f1);
+    g[1] = (p1 < P) ? g1 : 0.0;
+    if (p1 < P && !isfinite(g1)) bad = true;
+    fterm += f1;
+    gpl = fma(g[1], pdir[1], gpl);
   }
-  g = (p < P) ? gv : 0.0;
   double fs;
-  wave_sum2(fterm, g * pdir, fs, gp);
+  wave_sum2(fterm, gpl, fs, gp);
   f = fs + 0.5 * rrt * inv_s2;
-  bool bad = !isfinite(f);
-  if (p < P && !isfinite(gv)) bad = true;
+  if (!isfinite(f)) bad = true;
   return __ballot(bad) != 0ull;
 }
 
@@ -866,8 +912,9 @@ __device__ __forceinline__ bool eval_assemble(const FitKArgs &a, FitSmem<NW, KMA
 // (K2 / polish).  Every thread of the workgroup must call it.  `x` is this
 // lane's parameter (lane p < P); returns f in every thread and g (lane p).
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
-__device__ bool eval_collective(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, double x, double &f,
-                                double &g) {
+__device__ bool eval_collective(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm,
+                                const PV<ModeTr<MODE>::PW> &x, double &f, PV<ModeTr<MODE>::PW> &g) {
+  constexpr int PW = ModeTr<MODE>::PW;
   const int lane = pf_lane(), wave = pf_wave();
   PF_STAMP(0);
   publish_theta<NW, KMAX, MODE>(a, sm, x);
@@ -875,9 +922,11 @@ __device__ bool eval_collective(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, 
   eval_rows<NW, KMAX, O0, O1, O2, MODE>(a, sm);
   __syncthreads();
   if (wave == 0) {
-    double fw, gw, gpw;
-    const bool badw = eval_assemble<NW, KMAX, MODE>(a, sm, x, 0.0, fw, gw, gpw);
-    sm.gout[lane] = gw;
+    double fw, gpw;
+    PV<PW> gw;
+    const bool badw = eval_assemble<NW, KMAX, MODE>(a, sm, x, pv_zero<PW>(), fw, gw, gpw);
+#pragma unroll
+    for (int h = 0; h < PW; ++h) sm.gout[lane + 64 * h] = gw[h];
     if (lane == 0) {
       sm.fout[0] = fw;
       sm.fout[1] = badw ? 1.0 : 0.0;
@@ -885,10 +934,22 @@ __device__ bool eval_collective(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, 
   }
   __syncthreads();
   f = sm.fout[0];
-  g = sm.gout[lane];
+#pragma unroll
+  for (int h = 0; h < PW; ++h) g[h] = sm.gout[lane + 64 * h];
   const bool bad = sm.fout[1] != 0.0;
   __syncthreads();
   PF_STAMP(4);
+  return bad;
+}
+// single-word form (polish: P <= 64)
+template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
+__device__ __forceinline__ bool eval_collective1(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, double x,
+                                                 double &f, double &g) {
+  static_assert(ModeTr<MODE>::PW == 1, "polish is single-word");
+  PV<1> xv, gv;
+  xv[0] = x;
+  const bool bad = eval_collective<NW, KMAX, O0, O1, O2, MODE>(a, sm, xv, f, gv);
+  g = gv[0];
   return bad;
 }
 
@@ -912,13 +973,18 @@ __global__ __launch_bounds__(NW * 64) void k_objgrad(FitKArgs a) {
   FitSmem<NW, KMAX, MODE> sm;
   sm.carve(smem_raw, a.TQ, a.P);
   const int s = blockIdx.x, lane = pf_lane();
+  constexpr int PW = ModeTr<MODE>::PW;
   load_y<NW, KMAX, MODE>(a, sm, s);
-  const double x = (lane < a.P) ? a.theta[(size_t)s * a.P + lane] : 0.0;
+  PV<PW> x, g;
+#pragma unroll
+  for (int h = 0; h < PW; ++h) x[h] = (lane + 64 * h < a.P) ? a.theta[(size_t)s * a.P + lane + 64 * h] : 0.0;
   __syncthreads();
-  double f, g;
+  double f;
   const bool bad = eval_collective<NW, KMAX, O0, O1, O2, MODE>(a, sm, x, f, g);
   if (threadIdx.x < 64) {
-    if (lane < a.P) a.g_out[(size_t)s * a.P + lane] = g;
+#pragma unroll
+    for (int h = 0; h < PW; ++h)
+      if (lane + 64 * h < a.P) a.g_out[(size_t)s * a.P + lane + 64 * h] = g[h];
     if (lane == 0) a.f_out[s] = bad ? NAN : f;
   }
 }
@@ -975,7 +1041,13 @@ struct LbScalars {
   int itNum, resetB, nits, lsRestarts, zit, hcount, ret, n_eval, head;
 };
 
-__device__ __forceinline__ double ddot(double u, double v) { return wave_sum(u * v); }
+template <int PW>
+__device__ __forceinline__ double ddot(const PV<PW> &u, const PV<PW> &v) {
+  double s = u[0] * v[0];
+#pragma unroll
+  for (int h = 1; h < PW; ++h) s = fma(u[h], v[h], s);
+  return wave_sum(s);
+}
 // (a mod H) for 0 <= a < 2H without an integer division
 __device__ __forceinline__ int pf_wrap(int a, int H) {
   a = (a >= H) ? a - H : a;
@@ -984,9 +1056,10 @@ __device__ __forceinline__ int pf_wrap(int a, int H) {
 
 // Optimizer state kept in LDS (wave 0 only) so it does not compete with the
 // evaluation's registers.
+template <int PW>
 struct LbLds {
-  double xk[64], gk[64], pk[64];
-  double hs[PF_HIST][64], hy[PF_HIST][64];   // circular, logical j at (head + j) % H
+  double xk[64 * PW], gk[64 * PW], pk[64 * PW];        // parameter lane + 64 h at [lane + 64 h]
+  double hs[PF_HIST][64 * PW], hy[PF_HIST][64 * PW];   // circular, logical j at (head + j) % H
   // compact-form blocks in logical order (oldest = 0), zero beyond the
   // history length so the 5x5 solves run branch-free
   double Rm[PF_HIST][PF_HIST];                // Rm[i][j] = s_i . y_j (i <= j used)
@@ -1001,8 +1074,9 @@ struct LbLds {
 // Advance the machine until it needs an evaluation (returns true, trial point
 // in xq) or terminates (returns false).  `bad` / fq / gq are the result of the
 // evaluation requested last time.
-__device__ __forceinline__ bool lbfgs_step(const pf_fit_opts &o, LbLds &L, int &state, LbScalars &z,
-                                           double &xk, double &gk, double &pk, double &xq, double gq,
+template <int PW>
+__device__ __forceinline__ bool lbfgs_step(const pf_fit_opts &o, LbLds<PW> &L, int &state, LbScalars &z,
+                                           PV<PW> &xk, PV<PW> &gk, PV<PW> &pk, PV<PW> &xq, const PV<PW> &gq,
                                            double gpq, bool bad) {
   const int lane = pf_lane();
   const int H = o.history < PF_HIST ? o.history : PF_HIST;
@@ -1012,7 +1086,8 @@ __device__ __forceinline__ bool lbfgs_step(const pf_fit_opts &o, LbLds &L, int &
         if (bad) { z.ret = PF_ST_BADINIT; state = LB_DONE; return false; }
         z.fk = z.fq;
         gk = gq;
-        pk = -gk;
+#pragma unroll
+        for (int h = 0; h < PW; ++h) pk[h] = -gk[h];
         z.itNum = 0;
         z.hcount = 0;
         z.head = 0;
@@ -1032,7 +1107,8 @@ __device__ __forceinline__ bool lbfgs_step(const pf_fit_opts &o, LbLds &L, int &
           z.alpha = o.init_alpha;
         }
         if (z.resetB) {
-          pk = -gk;
+#pragma unroll
+          for (int h = 0; h < PW; ++h) pk[h] = -gk[h];
           z.dfp = ddot(gk, pk);
         } else {
           z.dfp = z.dfp_next;
@@ -1049,7 +1125,8 @@ __device__ __forceinline__ bool lbfgs_step(const pf_fit_opts &o, LbLds &L, int &
         break;
       case LB_TRY:
         if (z.nits >= 20) { state = LB_LS_FAIL; break; }
-        xq = xk + z.alpha1 * pk;
+#pragma unroll
+        for (int h = 0; h < PW; ++h) xq[h] = xk[h] + z.alpha1 * pk[h];
         state = LB_TRY_RES;
         return true;
       case LB_TRY_RES: {
@@ -1098,7 +1175,8 @@ __device__ __forceinline__ bool lbfgs_step(const pf_fit_opts &o, LbLds &L, int &
           if (z.alpha < lo + 0.01 * (hi - lo) || z.alpha > hi - 0.01 * (hi - lo))
             z.alpha = 0.5 * (z.alo + z.ahi);
         }
-        xq = xk + z.alpha * pk;
+#pragma unroll
+        for (int h = 0; h < PW; ++h) xq[h] = xk[h] + z.alpha * pk[h];
         state = LB_ZOOM_RES;
         return true;
       }
@@ -1107,7 +1185,8 @@ __device__ __forceinline__ bool lbfgs_step(const pf_fit_opts &o, LbLds &L, int &
           const double lo = fmin(z.alo, z.ahi);
           z.alpha = 0.5 * (z.alpha + lo);
           if (fabs(lo - z.alpha) < 1e-16) { state = LB_LS_FAIL; break; }
-          xq = xk + z.alpha * pk;
+#pragma unroll
+          for (int h = 0; h < PW; ++h) xq[h] = xk[h] + z.alpha * pk[h];
           return true;  // stay in LB_ZOOM_RES
         }
         const double f1 = z.fq;
@@ -1133,7 +1212,12 @@ __device__ __forceinline__ bool lbfgs_step(const pf_fit_opts &o, LbLds &L, int &
         // accepted point = last evaluated (xq, fq, gq); k becomes the newest
         z.fk1 = z.fk;
         z.fk = z.fq;
-        const double sk = xq - xk, yk = gq - gk;
+        PV<PW> sk, yk;
+#pragma unroll
+        for (int h = 0; h < PW; ++h) {
+          sk[h] = xq[h] - xk[h];
+          yk[h] = gq[h] - gk[h];
+        }
         xk = xq;
         gk = gq;
         z.alphak_1 = z.alpha;
@@ -1147,22 +1231,30 @@ __device__ __forceinline__ bool lbfgs_step(const pf_fit_opts &o, LbLds &L, int &
         // s_j.y, y_j.y of the kept pairs (their s_j.g, y_j.g follow by
         // a_j += s_j.y, b_j += y_j.y since g_new = g_old + y)
         double v[14], r[14];
-        v[0] = gq * gq;
-        v[1] = sk * sk;
-        v[2] = sk * yk;
-        v[3] = yk * yk;
-        v[4] = sk * gq;
-        v[5] = yk * gq;
+#pragma unroll
+        for (int i = 0; i < 14; ++i) v[i] = 0.0;
+#pragma unroll
+        for (int h = 0; h < PW; ++h) {
+          v[0] = fma(gq[h], gq[h], v[0]);
+          v[1] = fma(sk[h], sk[h], v[1]);
+          v[2] = fma(sk[h], yk[h], v[2]);
+          v[3] = fma(yk[h], yk[h], v[3]);
+          v[4] = fma(sk[h], gq[h], v[4]);
+          v[5] = fma(yk[h], gq[h], v[5]);
+        }
 #pragma unroll
         for (int j = 0; j < PF_HIST - 1; ++j) {
-          double sj = 0.0, yj = 0.0;
-          if (j < nw) {
-            const int slot = pf_wrap(z.head + j + drop, H);
-            sj = L.hs[slot][lane];
-            yj = L.hy[slot][lane];
+#pragma unroll
+          for (int h = 0; h < PW; ++h) {
+            double sj = 0.0, yj = 0.0;
+            if (j < nw) {
+              const int slot = pf_wrap(z.head + j + drop, H);
+              sj = L.hs[slot][lane + 64 * h];
+              yj = L.hy[slot][lane + 64 * h];
+            }
+            v[6 + 2 * j] = fma(sj, yk[h], v[6 + 2 * j]);
+            v[7 + 2 * j] = fma(yj, yk[h], v[7 + 2 * j]);
           }
-          v[6 + 2 * j] = sj * yk;
-          v[7 + 2 * j] = yj * yk;
         }
         wave_sum_multi<14>(v, r);
         PF_STAMP(11);
@@ -1173,7 +1265,7 @@ __device__ __forceinline__ bool lbfgs_step(const pf_fit_opts &o, LbLds &L, int &
           z.ret = PF_ST_ABSGRAD;
         } else if (sqrt(r[1]) < o.tol_param) {
           z.ret = PF_ST_ABSX;
-        } else if (z.itNum >= o.max_iter) {
+        } else if (z.itNum >= o.max_iter || (o.lbfgs_warmup_evals > 0 && z.n_eval >= o.lbfgs_warmup_evals)) {
           z.ret = PF_ST_MAXIT;
         } else if (((z.fk1 - z.fk) / fmax(fabs(z.fk1), fmax(fabs(z.fk), 1.0))) <
                    o.tol_rel_obj * 2.220446049250313e-16) {
@@ -1228,8 +1320,11 @@ __device__ __forceinline__ bool lbfgs_step(const pf_fit_opts &o, LbLds &L, int &
           }
           if (drop) z.head = pf_wrap(z.head + 1, H);
           const int slot_new = pf_wrap(z.head + nw, H);
-          L.hs[slot_new][lane] = sk;
-          L.hy[slot_new][lane] = yk;
+#pragma unroll
+          for (int h = 0; h < PW; ++h) {
+            L.hs[slot_new][lane + 64 * h] = sk[h];
+            L.hy[slot_new][lane + 64 * h] = yk[h];
+          }
           __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
           __builtin_amdgcn_wave_barrier();
           z.hcount = nw + 1;
@@ -1263,15 +1358,20 @@ __device__ __forceinline__ bool lbfgs_step(const pf_fit_opts &o, LbLds &L, int &
             for (int j = 0; j < i; ++j) w = fma(-Rr[j][i], pp[j], w);
             pp[i] = w * ri[i];
           }
-          double Hg = gam * gq;
+          PV<PW> Hg;
+#pragma unroll
+          for (int h = 0; h < PW; ++h) Hg[h] = gam * gq[h];
           double gHg = gam * gg;
 #pragma unroll
           for (int j = 0; j < PF_HIST; ++j) {
             const int sl = pf_wrap(z.head + j, H);
-            Hg = fma(pp[j], L.hs[sl][lane], fma(-gam * uu[j], L.hy[sl][lane], Hg));
+#pragma unroll
+            for (int h = 0; h < PW; ++h)
+              Hg[h] = fma(pp[j], L.hs[sl][lane + 64 * h], fma(-gam * uu[j], L.hy[sl][lane + 64 * h], Hg[h]));
             gHg = fma(pp[j], av[j], fma(-gam * uu[j], bv[j], gHg));
           }
-          pk = -Hg;
+#pragma unroll
+          for (int h = 0; h < PW; ++h) pk[h] = -Hg[h];
           z.dfp_next = -gHg;
           PF_STAMP(12);
           if (gHg / fmax(fabs(z.fk), 1.0) < o.tol_rel_grad * 2.220446049250313e-16)
@@ -1292,7 +1392,8 @@ __device__ __forceinline__ bool lbfgs_step(const pf_fit_opts &o, LbLds &L, int &
 
 // State lives in LDS between evaluations; copy it into registers for the
 // step (one batch of independent LDS loads) and write it back at the end.
-__device__ __forceinline__ bool lbfgs_advance(const pf_fit_opts &o, LbLds &L, double &xq, double gq,
+template <int PW>
+__device__ __forceinline__ bool lbfgs_advance(const pf_fit_opts &o, LbLds<PW> &L, PV<PW> &xq, const PV<PW> &gq,
                                               double gpq, bool bad) {
   const int lane = pf_lane();
   PF_STAMP(6);
@@ -1306,13 +1407,22 @@ __device__ __forceinline__ bool lbfgs_advance(const pf_fit_opts &o, LbLds &L, do
 #pragma unroll
     for (int i = 0; i < (int)(sizeof(LbScalars) / 4); ++i) w[i] = __builtin_amdgcn_readfirstlane(w[i]);
   }
-  double xk = L.xk[lane], gk = L.gk[lane], pk = L.pk[lane];
+  PV<PW> xk, gk, pk;
+#pragma unroll
+  for (int h = 0; h < PW; ++h) {
+    xk[h] = L.xk[lane + 64 * h];
+    gk[h] = L.gk[lane + 64 * h];
+    pk[h] = L.pk[lane + 64 * h];
+  }
   PF_STAMP(7);
-  const bool need = lbfgs_step(o, L, state, z, xk, gk, pk, xq, gq, gpq, bad);
+  const bool need = lbfgs_step<PW>(o, L, state, z, xk, gk, pk, xq, gq, gpq, bad);
   PF_STAMP(8);
-  L.xk[lane] = xk;
-  L.gk[lane] = gk;
-  L.pk[lane] = pk;
+#pragma unroll
+  for (int h = 0; h < PW; ++h) {
+    L.xk[lane + 64 * h] = xk[h];
+    L.gk[lane + 64 * h] = gk[h];
+    L.pk[lane + 64 * h] = pk[h];
+  }
   if (lane == 0) {
     L.z = z;
     L.state = state;
@@ -1320,7 +1430,6 @@ __device__ __forceinline__ bool lbfgs_advance(const pf_fit_opts &o, LbLds &L, do
   return need;
 }
 
-static_assert(sizeof(LbLds) + 16 <= kLbBytes, "LbLds too big");
 
 #include "pf_polish.h"
 
@@ -1348,16 +1457,23 @@ __device__ __forceinline__ void fit_body(const FitKArgs &a) {
     }
     return;
   }
+  constexpr int PW = ModeTr<MODE>::PW;
   load_y<NW, KMAX, MODE>(a, sm, s);
-  LbLds &L = *sm.lb;
-  double xq = (lane < P) ? th_out[lane] : 0.0;
+  LbLds<PW> &L = *sm.lb;
+  PV<PW> xq;
+#pragma unroll
+  for (int h = 0; h < PW; ++h) xq[h] = (lane + 64 * h < P) ? th_out[lane + 64 * h] : 0.0;
   if (pf_wave() == 0) {
     L.state = LB_INIT;
-    L.xk[lane] = xq;
     if (lane == 0) memset(&L.z, 0, sizeof(LbScalars));
 #pragma unroll
-    for (int q = 0; q < PF_HIST; ++q) { L.hs[q][lane] = 0.0; L.hy[q][lane] = 0.0; }
-    L.pk[lane] = 0.0;
+    for (int h = 0; h < PW; ++h) {
+      const int e = lane + 64 * h;
+      L.xk[e] = xq[h];
+      L.pk[e] = 0.0;
+#pragma unroll
+      for (int q = 0; q < PF_HIST; ++q) { L.hs[q][e] = 0.0; L.hy[q][e] = 0.0; }
+    }
     if (lane < PF_HIST * PF_HIST) { (&L.Rm[0][0])[lane] = 0.0; (&L.YYm[0][0])[lane] = 0.0; }
     if (lane < PF_HIST) { L.rinv[lane] = 0.0; L.av[lane] = 0.0; L.bv[lane] = 0.0; }
     publish_theta<NW, KMAX, MODE>(a, sm, xq);
@@ -1371,11 +1487,14 @@ __device__ __forceinline__ void fit_body(const FitKArgs &a) {
     eval_rows<NW, KMAX, O0, O1, O2, MODE>(a, sm);
     __syncthreads();
     if (pf_wave() == 0) {
-      double fq, gq, gpq;
-      const bool bad = eval_assemble<NW, KMAX, MODE>(a, sm, xq, L.pk[lane], fq, gq, gpq);
+      double fq, gpq;
+      PV<PW> gq, pkc;
+#pragma unroll
+      for (int h = 0; h < PW; ++h) pkc[h] = L.pk[lane + 64 * h];
+      const bool bad = eval_assemble<NW, KMAX, MODE>(a, sm, xq, pkc, fq, gq, gpq);
       ++n_eval;
       PF_STAMP(4);
-      if (lane == 0) L.z.fq = fq;
+      if (lane == 0) { L.z.fq = fq; L.z.n_eval = n_eval; }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
       const bool need = lbfgs_advance(a.o, L, xq, gq, gpq, bad);
@@ -1386,15 +1505,15 @@ __device__ __forceinline__ void fit_body(const FitKArgs &a) {
     PF_STAMP(5);
     if (!__builtin_amdgcn_readfirstlane(sm.flag[0])) break;
   }
-  double xk = L.xk[lane];
-  double gk = L.gk[lane];
   double f = L.z.fk;
   const double f_stan = f;
   int st_stan = L.z.ret;
   const int it_stan = L.z.itNum;
   if (a.warm_cap && st_stan == PF_ST_MAXIT) st_stan = PF_ST_WARMUP;
   if (threadIdx.x < 64) {
-    if (lane < P) th_out[lane] = xk;
+#pragma unroll
+    for (int h = 0; h < PW; ++h)
+      if (lane + 64 * h < P) th_out[lane + 64 * h] = L.xk[lane + 64 * h];
     if (lane == 0) {
       a.f_out[s] = f;
       if (a.pass == 0) {
@@ -1428,7 +1547,7 @@ __device__ __forceinline__ void polish_body(const FitKArgs &a) {
   double x = (lane < P) ? th_out[lane] : 0.0;
   __syncthreads();
   double f, g;
-  const bool bad = eval_collective<NW, KMAX, O0, O1, O2, MODE>(a, sm, x, f, g);
+  const bool bad = eval_collective1<NW, KMAX, O0, O1, O2, MODE>(a, sm, x, f, g);
   if (bad) return;
   int n_eval = 1, n_newton = 0;  // polish evaluations are not counted in n_eval[]
   const bool cert = polish_run<NW, KMAX, O0, O1, O2, MODE>(a, sm, x, f, g, n_eval, n_newton);
@@ -1477,7 +1596,7 @@ struct PredKArgs {
   uint32_t seed0, seed1;
   float *yhat, *ylo, *yhi, *tr, *trlo, *trhi, *mult, *add;
   int n_comp;
-  int comp_col0[4], comp_ncol[4];
+  int comp_col0[PF_MAX_COMP], comp_ncol[PF_MAX_COMP];
   float *comp;
   const uint32_t *series_id;  // RNG stream key per series (NULL: batch index)
   int method;                 // PF_INTERVAL_EXACT / PF_INTERVAL_SAMPLE
@@ -1502,6 +1621,7 @@ __device__ __forceinline__ void pred_setup(const PredKArgs &a, int series, PredS
   if (pf_wave() != 0) return;
   const int P = a.P, S = a.S, K = a.K;
   const double x = (lane < P) ? a.theta[(size_t)series * P + lane] : 0.0;
+  const double x1 = (lane + 64 < P) ? a.theta[(size_t)series * P + 64 + lane] : 0.0;  // P > 64: betas
   const double k = readlane_f64(x, 0), m = readlane_f64(x, 1);
   const double dj = __shfl(x, (lane + 2) & 63, 64);
   const double dval = (lane < S) ? dj : 0.0;
@@ -1519,7 +1639,8 @@ __device__ __forceinline__ void pred_setup(const PredKArgs &a, int series, PredS
     ps.kseg[lane] = kl;
     ps.mseg[lane] = m - (lane == 0 ? 0.0 : ctd_ex);
   }
-  const double bval = __shfl(x, (lane + 3 + S) & 63, 64);
+  const double b0 = __shfl(x, (lane + 3 + S) & 63, 64), b1 = __shfl(x1, (lane + 3 + S) & 63, 64);
+  const double bval = (lane + 3 + S < 64) ? b0 : b1;
   const double bv = (lane < K) ? bval : 0.0;
   ps.bm[lane] = bv * ((lane < K) ? a.s_m[lane] : 0.0);
   ps.ba[lane] = bv * ((lane < K) ? a.s_a[lane] : 0.0);
@@ -1567,21 +1688,23 @@ __global__ __launch_bounds__(256) void k_predict_det(PredKArgs a) {
   const double ti = a.t[row];
   const int sg = a.seg[row];
   double xbm = 0.0, xba = 0.0;
-  double cb[4] = {0.0, 0.0, 0.0, 0.0};
   for (int f = 0; f < a.K; ++f) {
     const double xv = a.XT[(size_t)f * a.Tp + row];
-    const double pm = xv * ps.bm[f], pa = xv * ps.ba[f];
-    xbm += pm;
-    xba += pa;
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-      if (b < a.n_comp && f >= a.comp_col0[b] && f < a.comp_col0[b] + a.comp_ncol[b])
-        cb[b] += pm + pa * ysc;
+    xbm += xv * ps.bm[f];
+    xba += xv * ps.ba[f];
   }
   if (a.comp) {
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-      if (b < a.n_comp) a.comp[((size_t)b * a.n_series + series) * a.Tp + row] = (float)cb[b];
+    // component blocks: contiguous column ranges (UPSTREAM
+    // predict_seasonal_components, MAP: the mean); additive parts x y_scale
+    for (int b = 0; b < a.n_comp; ++b) {
+      double cb = 0.0;
+      const int c0 = a.comp_col0[b], c1 = c0 + a.comp_ncol[b];
+      for (int f = c0; f < c1; ++f) {
+        const double xv = a.XT[(size_t)f * a.Tp + row];
+        cb += xv * ps.bm[f] + xv * ps.ba[f] * ysc;
+      }
+      a.comp[((size_t)b * a.n_series + series) * a.Tp + row] = (float)cb;
+    }
   }
   const double trs = pred_trend(a, ps, series, row, ti, sg);
   const double trend = trs * ysc;
@@ -1715,7 +1838,7 @@ void pf_default_fit_opts(pf_fit_opts *o) {
   o->polish = 1;
   o->polish_max_iter = 20;
   o->lbfgs_warmup = 60;
-  o->_pad = 0;
+  o->lbfgs_warmup_evals = 0;
 }
 
 int pf_num_changepoints(int T, int n_changepoints, double changepoint_range) {
@@ -1877,6 +2000,7 @@ int launch_fitlike(pf_ctx *ctx, bool fit, const FitKArgs &a, int n, hipStream_t 
       FitKArgs b = a;
       b.o.max_iter = caps[ps];
       b.warm_cap = warm[ps];
+      if (!warm[ps]) b.o.lbfgs_warmup_evals = 0;
       b.pass = ps;
       const int v = ps == 0 ? 0 : 1;
       PF_TIMED_LAUNCH(ctx, v ? "k_fit_resume" : "k_fit", n, st, kf[v], dim3(n), dim3(NW * 64),
@@ -1908,7 +2032,21 @@ int dispatch_fitlike(pf_ctx *ctx, bool fit, const FitKArgs &a, int n, const int3
                      hipStream_t st) {
   const bool o1030 = orders[0] == 10 && orders[1] == 3 && orders[2] == 0;
   const bool o1034 = orders[0] == 10 && orders[1] == 3 && orders[2] == 4;
-  constexpr int LG = PF_MODE_LOGI;
+  constexpr int LG = PF_MODE_LOGI, WD = PF_MODE_WIDE;
+  // extra (holiday / regressor) columns after the Fourier blocks: up to 10
+  // with yearly + weekly (P <= 64), up to 10 with yearly + weekly + daily
+  // (P <= 72: two parameter words per lane) — SURVEY.md §8d configs[4]
+  if (o1030 && a.K > 26 && a.K <= 36 && mode == MODE_MULT) {
+    if (a.growth == PF_GROWTH_LOGISTIC)
+      return launch_fitlike<PF_FIT_NW, 36, 10, 3, 0, MODE_MULT | LG>(ctx, fit, a, n, st);
+    return launch_fitlike<PF_FIT_NW, 36, 10, 3, 0, MODE_MULT>(ctx, fit, a, n, st);
+  }
+  if (o1034 && a.K > 34 && a.K <= 44 && mode == MODE_MULT) {
+    if (a.growth == PF_GROWTH_LOGISTIC)
+      return launch_fitlike<PF_FIT_NW, 44, 10, 3, 4, MODE_MULT | LG | WD>(ctx, fit, a, n, st);
+    return launch_fitlike<PF_FIT_NW, 44, 10, 3, 4, MODE_MULT | WD>(ctx, fit, a, n, st);
+  }
+  if (a.P > 64) return set_err(ctx, "fit: P > 64 is supported for yearly+weekly+daily (10,3,4) plus <= 10 extra columns, multiplicative");
   if (a.growth == PF_GROWTH_LOGISTIC) {
     if (o1030 && a.K == 26 && mode == MODE_MULT)
       return launch_fitlike<PF_FIT_NW, 26, 10, 3, 0, MODE_MULT | LG>(ctx, fit, a, n, st);
@@ -1966,7 +2104,7 @@ static int check_problem(pf_ctx *ctx, const pf_problem *pb) {
   if (pb->growth == PF_GROWTH_LOGISTIC && !pb->cap_scaled)
     return set_err(ctx, "logistic growth needs cap_scaled");
   const int P = 3 + pb->grid.S + pb->grid.K;
-  if (P > 64) return set_err(ctx, "P = 3 + S + K must be <= 64 on this build");
+  if (P > 128) return set_err(ctx, "P = 3 + S + K must be <= 128");
   if (pb->grid.S < 1 || pb->grid.S > 62) return set_err(ctx, "S out of range");
   if (pb->grid.T < 2 || pb->grid.T_pad % 128) return set_err(ctx, "bad T / T_pad");
   if (!pb->grid.t || !pb->grid.XT || !pb->grid.t_change || !pb->grid.seg || !pb->sigmas ||
@@ -2016,7 +2154,7 @@ int pf_predict(pf_ctx *ctx, const pf_predict_args *p, void *stream) {
   if (!p) return set_err(ctx, "pf_predict: NULL args");
   if (p->n_samples < 0 || p->n_samples > 64 * PF_NQ) return set_err(ctx, "pf_predict: n_samples must be in [0, 1024]");
   const int P = 3 + p->fg.S + p->fg.K;
-  if (P > 64 || p->fg.K > 64) return set_err(ctx, "pf_predict: P must be <= 64");
+  if (P > 128 || p->fg.K > 64) return set_err(ctx, "pf_predict: P must be <= 128 and K <= 64");
   if (!p->fg.t || !p->fg.XT || !p->fg.t_change || !p->fg.seg || !p->theta || !p->y_scale ||
       !p->yhat || !p->yhat_lower || !p->yhat_upper)
     return set_err(ctx, "pf_predict: NULL buffer");
@@ -2055,8 +2193,10 @@ int pf_predict(pf_ctx *ctx, const pf_predict_args *p, void *stream) {
   a.comp = p->comp;
   a.series_id = p->series_id;
   a.n_comp = p->comp ? p->n_comp : 0;
-  if (a.n_comp < 0 || a.n_comp > 4) return set_err(ctx, "pf_predict: n_comp must be in [0, 4]");
-  for (int b = 0; b < 4; ++b) {
+  if (a.n_comp < 0 || a.n_comp > PF_MAX_COMP) return set_err(ctx, "pf_predict: n_comp must be in [0, PF_MAX_COMP]");
+  for (int b = 0; b < a.n_comp; ++b) {
+    if (p->comp_col0[b] < 0 || p->comp_ncol[b] < 0 || p->comp_col0[b] + p->comp_ncol[b] > p->fg.K)
+      return set_err(ctx, "pf_predict: component block outside [0, K)");
     a.comp_col0[b] = p->comp_col0[b];
     a.comp_ncol[b] = p->comp_ncol[b];
   }

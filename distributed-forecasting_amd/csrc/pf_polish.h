@@ -37,15 +37,17 @@ __device__ __forceinline__ int colmap(int c, int S, int K) {
 }
 
 // publish theta (wave 0) — same as the evaluation's phase 0
-template <int NW, int KMAX, int MODE>
-__device__ __forceinline__ void publish_theta(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, double x);
 
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
 __device__ __forceinline__ void hessian_collective(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, double x,
                                    double gh, double *ws) {
   const int lane = pf_lane(), wave = pf_wave();
   const int S = a.S, K = a.K, T = a.T, Tp = a.Tp, P = a.P;
-  publish_theta<NW, KMAX, MODE>(a, sm, x);
+  {
+    PV<1> xv;
+    xv[0] = x;
+    publish_theta<NW, KMAX, MODE>(a, sm, xv);
+  }
   __syncthreads();
   // ---- H1: per-row u, tr, r into the workspace (row per lane)
   double Q = 0.0;
@@ -497,7 +499,7 @@ __device__ __forceinline__ bool polish_run(const FitKArgs &a, FitSmem<NW, KMAX, 
     bool acc = false;
     for (int ls = 0; ls < 30; ++ls) {
       xn = x + alpha * d;
-      const bool bad = eval_collective<NW, KMAX, O0, O1, O2, MODE>(a, sm, xn, fn, gn);
+      const bool bad = eval_collective1<NW, KMAX, O0, O1, O2, MODE>(a, sm, xn, fn, gn);
       ++n_eval;
       if (!bad && fn <= f + 1e-4 * alpha * dec) { acc = true; break; }
       alpha *= 0.5;

@@ -21,6 +21,7 @@ import numpy as np
 import torch
 
 from . import _lib as L
+from .holidays import HolidaySpec, holiday_columns
 
 NS_PER_DAY = 86400 * 10**9
 
@@ -152,6 +153,7 @@ class DeviceGrid:
     cp_first: torch.Tensor
     cp_idx: torch.Tensor | None = None
     n_changepoints_placed: int = 0
+    holidays: HolidaySpec | None = None   # extra 0/1 columns after the Fourier blocks
 
     def as_pf(self) -> L.PfGrid:
         return L.PfGrid(self.T, self.T_pad, self.K, self.S, self.t.data_ptr(), self.XT.data_ptr(),
@@ -167,14 +169,19 @@ class DeviceGrid:
 
 def build_grid(ds_ns: np.ndarray, seasons, *, start_ns: int, t_scale_ns: int,
                n_changepoints: int = 25, changepoint_range: float = 0.8,
-               t_change: torch.Tensor | None = None, device: int = 0) -> DeviceGrid:
+               t_change: torch.Tensor | None = None, device: int = 0,
+               holidays: HolidaySpec | None = None) -> DeviceGrid:
     """Design grid on the GPU (K1).  With ``t_change=None`` the changepoints are
-    placed (fit grid); otherwise they are reused (predict grid)."""
+    placed (fit grid); otherwise they are reused (predict grid).  ``holidays``
+    appends its indicator columns after the Fourier blocks (UPSTREAM
+    make_all_seasonality_features order)."""
     ctx = Context.get(device)
     ds_ns = np.ascontiguousarray(np.asarray(ds_ns, dtype=np.int64))
     T = int(ds_ns.shape[0])
     Tp = pad_rows(T)
     K = sum(2 * o for _, _, o in seasons)
+    n_extra = holidays.n if holidays is not None else 0
+    K += n_extra
     if K == 0:
         raise ValueError("no seasonality columns: the zero-feature dummy X is not supported yet")
     dev = torch.device("cuda", device)
@@ -199,13 +206,37 @@ def build_grid(ds_ns: np.ndarray, seasons, *, start_ns: int, t_scale_ns: int,
         ncp = -1
         S_eff = S
     cp_first = torch.empty(S, dtype=torch.int32, device=dev)
+    extra = None
+    if n_extra:
+        extra = torch.from_numpy(np.ascontiguousarray(holiday_columns(holidays, ds_ns))).to(dev)
     rc = ctx.lib.pf_build_grid(ctx.h, _ptr(ds_d), T, Tp, int(start_ns), int(t_scale_ns), sp,
-                               len(seasons), None, 0, ncp, float(changepoint_range), _ptr(t),
+                               len(seasons), _ptr(extra), n_extra, ncp, float(changepoint_range), _ptr(t),
                                _ptr(XT), _ptr(tc), _ptr(cp_idx), _ptr(seg), _ptr(cp_first), S,
                                _stream(device))
     ctx.check(rc, "pf_build_grid")
     return DeviceGrid(ds_ns, int(start_ns), int(t_scale_ns), list(seasons), T, Tp, K, S, t, XT,
-                      tc, seg, cp_first, cp_idx, S_eff)
+                      tc, seg, cp_first, cp_idx, S_eff, holidays if n_extra else None)
+
+
+def component_blocks(grid: DeviceGrid):
+    """[(name, first column, n columns)] of Prophet's predicted components
+    (UPSTREAM regressor_column_matrix): each seasonality; each holiday (its
+    window columns) and 'holidays' (all of them).  At most PF_MAX_COMP."""
+    out, col = [], 0
+    for name, _, order in grid.seasons:
+        out.append((name, col, 2 * order))
+        col += 2 * order
+    h = grid.holidays
+    if h is not None and h.n:
+        h0 = col
+        for hn in sorted(set(k.split("_delim_")[0] for k in h.names)):
+            idx = [i for i, k in enumerate(h.names) if k.split("_delim_")[0] == hn]
+            assert idx == list(range(idx[0], idx[-1] + 1)), "holiday columns not contiguous"
+            out.append((hn, h0 + idx[0], len(idx)))
+        out.append(("holidays", h0, h.n))
+    if len(out) > L.PF_MAX_COMP:
+        raise ValueError(f"more than {L.PF_MAX_COMP} components")
+    return out
 
 
 def future_dates(history_dates_ns: np.ndarray, periods: int, freq_ns: int = NS_PER_DAY,
@@ -249,15 +280,25 @@ class Engine:
     # prior scales and mode indicators (UPSTREAM regressor_column_matrix)
     def _vectors(self, grid: DeviceGrid):
         key = (grid.K, tuple(grid.seasons), self.config.seasonality_mode,
-               self.config.seasonality_prior_scale)
+               self.config.seasonality_prior_scale, grid.holidays)
         if key not in self._vec_cache:
             dev = torch.device("cuda", self.device)
+            h = grid.holidays
+            nh = h.n if h is not None else 0
+            ks = grid.K - nh
             mult = self.config.seasonality_mode == "multiplicative"
-            sig = torch.full((grid.K,), float(self.config.seasonality_prior_scale),
-                             dtype=torch.float64, device=dev)
-            s_m = torch.full((grid.K,), 1.0 if mult else 0.0, dtype=torch.float64, device=dev)
-            s_a = torch.full((grid.K,), 0.0 if mult else 1.0, dtype=torch.float64, device=dev)
-            self._vec_cache[key] = (sig, s_a, s_m, 0 if mult else 1)
+            sig = [float(self.config.seasonality_prior_scale)] * ks
+            m = [1.0 if mult else 0.0] * ks
+            if nh:
+                hm = h.mode == "multiplicative"
+                sig += [float(v) for v in h.prior_scales]
+                m += [1.0 if hm else 0.0] * nh
+            m = np.asarray(m)
+            code = 0 if np.all(m == 1.0) else (1 if np.all(m == 0.0) else 2)
+            sig_t = torch.tensor(sig, dtype=torch.float64, device=dev)
+            s_m = torch.tensor(m, dtype=torch.float64, device=dev)
+            s_a = 1.0 - s_m
+            self._vec_cache[key] = (sig_t, s_a, s_m, code)
         return self._vec_cache[key]
 
     def problem(self, grid: DeviceGrid, y_scaled: torch.Tensor, n: int,
@@ -363,7 +404,7 @@ class Engine:
         g = fit.grid
         return build_grid(ds_ns, g.seasons, start_ns=g.start_ns, t_scale_ns=g.t_scale_ns,
                           changepoint_range=self.config.changepoint_range, t_change=g.t_change,
-                          device=self.device)
+                          device=self.device, holidays=getattr(g, "holidays", None))
 
     def predict(self, fit: FitResult, fgrid: DeviceGrid, n_samples: int | None = None,
                 seed: int = 0, components: bool = True,
@@ -414,18 +455,15 @@ class Engine:
                                                      ("trend", "trend_lower", "trend_upper"))
             a.mult_terms = out["multiplicative_terms"].data_ptr()
             a.add_terms = out["additive_terms"].data_ptr()
-        if components and fgrid.seasons:
-            nb = min(4, len(fgrid.seasons))
-            comp = torch.empty((nb, n, fgrid.T_pad), dtype=torch.float32, device=dev)
-            col = 0
-            for b, (_, _, order) in enumerate(fgrid.seasons[:nb]):
-                a.comp_col0[b] = col
-                a.comp_ncol[b] = 2 * order
-                col += 2 * order
-            a.n_comp = nb
-            a.comp = comp.data_ptr()
-            for b, (name, _, _) in enumerate(fgrid.seasons[:nb]):
+        blocks = component_blocks(fgrid) if components else []
+        if blocks:
+            comp = torch.empty((len(blocks), n, fgrid.T_pad), dtype=torch.float32, device=dev)
+            for b, (name, c0, nc) in enumerate(blocks):
+                a.comp_col0[b] = c0
+                a.comp_ncol[b] = nc
                 out[name] = comp[b]
+            a.n_comp = len(blocks)
+            a.comp = comp.data_ptr()
         if series_id is not None:
             assert series_id.numel() == n and series_id.dtype == torch.int32 and series_id.is_cuda
             a.series_id = series_id.data_ptr()

@@ -10,10 +10,11 @@ that surface; ``fit`` is a batch of one through the same kernels the batched
 entry points use.
 
 Supported: linear, flat and logistic growth (capacity column 'cap', floor 0),
+holidays (frame with holiday / ds / lower_window / upper_window / prior_scale),
 auto/True/False/int seasonalities
 (yearly, weekly, daily), additive and multiplicative seasonality, MAP fit,
 ``uncertainty_samples`` up to 1024.  Not supported yet (raise
-NotImplementedError): logistic floor, holidays, extra regressors, custom
+NotImplementedError): logistic floor, extra regressors, custom
 seasonalities, user-specified changepoints, ``mcmc_samples > 0``.
 """
 from __future__ import annotations
@@ -24,6 +25,7 @@ import torch
 
 from . import batch as B
 from . import engine as E
+from . import holidays as H
 
 # UPSTREAM serialize.SIMPLE_ATTRIBUTES (what 02_training.py:146-147 logs)
 SIMPLE_ATTRIBUTES = [
@@ -68,7 +70,8 @@ class Prophet:
         if changepoints is not None:
             raise NotImplementedError("user-specified changepoints are not supported yet")
         if holidays is not None:
-            raise NotImplementedError("holidays are not supported yet")
+            # UPSTREAM validate_inputs: checked now, columns built at fit
+            H.holiday_spec(holidays, float(holidays_prior_scale))
         if mcmc_samples:
             raise NotImplementedError("mcmc_samples > 0 (full posterior) is not supported")
         if seasonality_mode not in ("additive", "multiplicative"):
@@ -81,7 +84,8 @@ class Prophet:
         self.yearly_seasonality = yearly_seasonality
         self.weekly_seasonality = weekly_seasonality
         self.daily_seasonality = daily_seasonality
-        self.holidays = None
+        self.holidays = None if holidays is None else holidays.copy()
+        self.train_holiday_names = None
         self.seasonality_mode = seasonality_mode
         self.seasonality_prior_scale = float(seasonality_prior_scale)
         self.holidays_prior_scale = float(holidays_prior_scale)
@@ -150,9 +154,14 @@ class Prophet:
             cap = history["cap"].to_numpy(np.float64)[order][None, :]
             if np.any(cap <= 0.0):
                 raise ValueError("Cap must be greater than floor (which defaults to 0).")
+        spec = None
+        if self.holidays is not None and len(self.holidays):
+            # Prophet 1.0: holiday columns follow seasonality_mode
+            spec = H.holiday_spec(self.holidays, self.holidays_prior_scale, self.seasonality_mode)
+            self.train_holiday_names = pd.Series(list(spec.holidays))
         eng = get_engine(self.config(), self.device)
         fb = B.FittedBatch.fit_dense(eng, ds, y[None, :], history_dates=all_ds,
-                                     series_ids=np.array([0], np.int32), cap=cap)
+                                     series_ids=np.array([0], np.int32), cap=cap, holidays=spec)
         self._attach(fb, history=history.iloc[order].reset_index(drop=True))
         self.fit_kwargs = dict(kwargs)
         return self
@@ -183,6 +192,10 @@ class Prophet:
                                      self.seasonality_prior_scale, "mode": mode,
                                      "condition_name": None} for name, p, o in g.seasons}
         names = [s[0] for s in g.seasons]
+        hspec = getattr(g, "holidays", None)
+        if hspec is not None:
+            names += list(hspec.holidays)
+            self.holidays_prior_scales = dict(zip(hspec.names, hspec.prior_scales))
         add = [] if mode == "multiplicative" else list(names)
         mul = list(names) if mode == "multiplicative" else []
         add += ["additive_terms", "extra_regressors_additive"]
@@ -245,6 +258,9 @@ def predict_frame(fb: B.FittedBatch, row: int, ds: np.ndarray, mode: str, seed: 
                              cap=None if cap is None else np.asarray(cap)[None, :])
     host = {k: v[row, :Tf].cpu().numpy() for k, v in out.items()}
     names = [s[0] for s in fb.fit.grid.seasons]
+    hspec = getattr(fb.fit.grid, "holidays", None)
+    if hspec is not None and hspec.n:
+        names += sorted(set(hspec.holidays)) + ["holidays"]
     cols = {"ds": ds.astype("datetime64[ns]"), "trend": host["trend"]}
     if cap is not None:
         cols["cap"] = np.asarray(cap, np.float64)

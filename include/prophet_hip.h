@@ -97,9 +97,14 @@ typedef struct {
    * series whose polish does not certify convergence resumes L-BFGS (once
    * more for lbfgs_warmup iterations, then with Stan's full termination
    * rules) and is polished again.  0 = run Stan's full termination rules
-   * first (the reference's behaviour), then polish.                        */
-  int32_t lbfgs_warmup, _pad;
+   * first (the reference's behaviour), then polish.  lbfgs_warmup_evals > 0
+   * also ends a warm-up pass once it has used that many evaluations (at the
+   * next accepted iterate).                                                  */
+  int32_t lbfgs_warmup, lbfgs_warmup_evals;
 } pf_fit_opts;
+
+/* component blocks pf_predict can report (seasonalities, holidays, ...) */
+#define PF_MAX_COMP 32
 
 /* ---------------------------------------------------------------- context */
 int pf_ctx_create(int device, pf_ctx **out);
@@ -196,7 +201,7 @@ typedef struct {
    * block b covers columns [comp_col0[b], comp_col0[b]+comp_ncol[b]); output
    * comp[(b*n + s)*T_pad + row] (additive blocks already x y_scale).      */
   int32_t n_comp;
-  int32_t comp_col0[4], comp_ncol[4];
+  int32_t comp_col0[PF_MAX_COMP], comp_ncol[PF_MAX_COMP];
   float *comp;
   /* optional [n_series] RNG stream key per series (e.g. a hash of
    * (store, item)) so samples do not depend on batch position; NULL: use

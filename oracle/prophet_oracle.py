@@ -34,6 +34,7 @@ import math
 from dataclasses import dataclass, field
 
 import numpy as np
+import pandas as pd
 
 NS_PER_DAY = 86400 * 10**9
 EPOCH_NS = 0  # 1970-01-01 in datetime64[ns]
@@ -167,6 +168,28 @@ def make_features(ds_ns, cfg=None, holiday_cols=None):
     s_m = np.full(F, 1.0 if mult else 0.0)
     s_a = np.full(F, 0.0 if mult else 1.0)
     return X, np.asarray(sig, np.float64), s_a, s_m
+
+
+def holiday_features(ds_ns, holidays):
+    """UPSTREAM make_holiday_features (Prophet 1.0 forecaster.py): for each
+    holiday row and offset in [lower_window, upper_window], a column keyed
+    '{holiday}_delim_{+|-}{|offset|}' set to 1 on the rows whose date
+    (``dates.dt.date``) equals the holiday date + offset; columns sorted by key.
+    Returns (X [T x n], keys)."""
+    dates = pd.to_datetime(np.asarray(ds_ns, np.int64)).normalize()
+    cols = {}
+    for row in holidays.itertuples(index=False):
+        dt = pd.Timestamp(row.ds).normalize()
+        lw = int(getattr(row, "lower_window", 0))
+        uw = int(getattr(row, "upper_window", 0))
+        for offset in range(lw, uw + 1):
+            occ = dt + pd.Timedelta(days=offset)
+            key = "{}_delim_{}{}".format(row.holiday, "+" if offset >= 0 else "-", abs(offset))
+            col = cols.setdefault(key, np.zeros(len(dates)))
+            col[dates == occ] = 1.0
+    keys = sorted(cols)
+    X = np.column_stack([cols[k] for k in keys]) if keys else np.zeros((len(dates), 0))
+    return X, keys
 
 
 # ----------------------------------------------------------------------------

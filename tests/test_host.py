@@ -60,6 +60,34 @@ def test_logistic_requires_cap():
         dfa.Prophet(growth="logistic").fit(d2)
 
 
+def test_holiday_columns_match_oracle():
+    """UPSTREAM make_holiday_features: window offsets, date matching of every
+    hourly row of the day, '_delim_' keys sorted, same columns at predict."""
+    import pandas as pd
+    from distributed_forecasting_amd import holidays as H
+    ds = synthetic.hourly_dates(n_hours=24 * 400)
+    hd = pd.concat([H.synthetic_holidays([2016, 2017, 2018]),
+                    pd.DataFrame({"holiday": ["xmas"], "ds": [pd.Timestamp("2016-12-25")],
+                                  "lower_window": [-2], "upper_window": [1]})])
+    spec = H.holiday_spec(hd, 10.0)
+    X = H.holiday_columns(spec, ds)
+    Xo, keys = po.holiday_features(ds, hd)
+    assert list(spec.names) == keys and len(keys) == 14
+    assert np.array_equal(X.T, Xo)
+    assert "xmas_delim_-2" in keys and X.sum() > 0
+
+
+def test_holiday_spec_errors():
+    import pandas as pd
+    from distributed_forecasting_amd import holidays as H
+    hd = pd.DataFrame({"holiday": ["a", "a"], "ds": pd.to_datetime(["2016-01-01", "2017-01-01"]),
+                       "prior_scale": [1.0, 2.0]})
+    with pytest.raises(ValueError, match="consistent prior scale"):
+        H.holiday_spec(hd)
+    with pytest.raises(ValueError, match="both lower_window and upper_window"):
+        H.holiday_spec(hd.drop(columns="prior_scale").assign(lower_window=0))
+
+
 def test_seasonality_auto_rules():
     cfg = ProphetConfig()
     d = NS_PER_DAY
