@@ -1562,12 +1562,19 @@ __device__ __forceinline__ void polish_body(const FitKArgs &a) {
 
 // Entry points: the first pass and the resume passes are distinct kernels so
 // that traces and counters attribute them separately.
+// waves per SIMD the register budget targets: 2 for the reference layouts; 1
+// (512 registers, no spills) for the holiday / wide layouts, whose long
+// (hourly) grids hold one workgroup per CU in LDS anyway
+template <int KMAX>
+struct FitOcc {
+  static constexpr int W = KMAX > 34 ? 1 : 2;
+};
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
-__global__ __launch_bounds__(NW * 64, 2) void k_fit(FitKArgs a) {
+__global__ __launch_bounds__(NW * 64, FitOcc<KMAX>::W) void k_fit(FitKArgs a) {
   fit_body<NW, KMAX, O0, O1, O2, MODE>(a);
 }
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
-__global__ __launch_bounds__(NW * 64, 2) void k_fit_resume(FitKArgs a) {
+__global__ __launch_bounds__(NW * 64, FitOcc<KMAX>::W) void k_fit_resume(FitKArgs a) {
   fit_body<NW, KMAX, O0, O1, O2, MODE>(a);
 }
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>

@@ -1,0 +1,120 @@
+"""Throughput on the other BASELINE.json configurations (1 GPU), as JSON lines.
+
+  python tools/bench_configs.py 3 [n]   # configs[2]: n (50k) x 1826-day daily series
+  python tools/bench_configs.py 4 [n]   # configs[3]: n (1M) x 730 days, full MC intervals
+  python tools/bench_configs.py 5 [n]   # configs[4]: n x 8760 hourly, logistic + cap,
+                                         # daily+weekly+yearly + 10 holidays/yr (P = 72)
+
+The headline (configs[1]) is bench.py.  Each run: synthetic data resident in
+HBM, one untimed warm-up chunk, then the whole workload timed (fit + forecast
++ intervals), in chunks of at most --chunk series per launch.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("config", type=int, choices=[3, 4, 5])
+    ap.add_argument("n", type=int, nargs="?", default=None)
+    ap.add_argument("--chunk", type=int, default=None)
+    ap.add_argument("--method", default=None, help="interval method (default per config)")
+    args = ap.parse_args()
+    import torch
+    import distributed_forecasting_amd as dfa
+    from distributed_forecasting_amd import batch as B, holidays as H, synthetic
+    from distributed_forecasting_amd.engine import ProphetConfig
+
+    cfg = ProphetConfig.reference()
+    hol = None
+    cap = None
+    if args.config == 3:
+        n = args.n or 50_000
+        ds = synthetic.daily_dates()
+        Y = synthetic.sales_matrix(n, ds, config_index=2)
+        seasons = cfg.seasons(int(ds[0]), int(ds[-1]), int(ds[1] - ds[0]))
+        horizon, step_ns, method, chunk = 90, synthetic.NS_PER_DAY, args.method or "exact", args.chunk or 50_000
+        work = f"configs[2]: {n} series x 1826 days (yearly+weekly), 90-day forecast, 1000-sample intervals"
+    elif args.config == 4:
+        n = args.n or 1_000_000
+        ds = synthetic.daily_dates("2016-01-01", "2017-12-30")
+        Y = synthetic.sales_matrix(n, ds, config_index=3)
+        seasons = cfg.seasons(int(ds[0]), int(ds[-1]), int(ds[1] - ds[0]))
+        horizon, step_ns, method, chunk = 90, synthetic.NS_PER_DAY, args.method or "sample", args.chunk or 125_000
+        work = (f"configs[3]: {n} series x 730 days, 25 changepoints, 90-day forecast, full MC "
+                f"intervals (interval_method={method}: every row's 1000 samples materialised)")
+    else:
+        n = args.n or 20_000
+        ds = synthetic.hourly_dates(n_hours=8760)
+        Y, cap = synthetic.saturating_matrix(n, ds)
+        cfg.growth = "logistic"
+        seasons = [("yearly", 365.25, 10), ("weekly", 7.0, 3), ("daily", 1.0, 4)]
+        hol = H.holiday_spec(H.synthetic_holidays([2017, 2018]), cfg.holidays_prior_scale,
+                             cfg.seasonality_mode)
+        horizon, step_ns, method, chunk = 90, synthetic.NS_PER_HOUR, args.method or "exact", args.chunk or 10_000
+        work = (f"configs[4]: {n} hourly series x 8760 steps, logistic growth (cap = 1.2 max y), "
+                f"daily+weekly+yearly + 10 holidays/yr (K = 44, P = 72), 90-step forecast, "
+                f"1000-sample intervals")
+    eng = dfa.Engine(0, cfg)
+    dev = torch.device("cuda", 0)
+    T = len(ds)
+    grid = dfa.build_grid(ds, seasons, start_ns=int(ds[0]), t_scale_ns=int(ds[-1] - ds[0]), holidays=hol)
+    Tp = grid.T_pad
+    fut = np.concatenate([ds, ds[-1] + step_ns * np.arange(1, horizon + 1)])
+    chunks = [(i, min(n, i + chunk)) for i in range(0, n, chunk)]
+    # inputs resident in HBM before the timed region
+    Yd = [torch.zeros((b - a, Tp), dtype=torch.float64, device=dev) for a, b in chunks]
+    for (a, b), t in zip(chunks, Yd):
+        t[:, :T] = torch.from_numpy(Y[a:b]).to(dev)
+    capd = capf = None
+    if cap is not None:
+        capd = []
+        for (a, b) in chunks:
+            c = torch.zeros((b - a, Tp), dtype=torch.float64, device=dev)
+            c[:, :T] = torch.from_numpy(cap[a:b]).to(dev)
+            capd.append(c)
+    sid = [torch.arange(a, b, dtype=torch.int32, device=dev) for a, b in chunks]
+
+    def run(k):
+        fit = eng.fit(grid, Yd[k], cap=None if capd is None else capd[k])
+        fg = eng.predict_grid(fit, fut)
+        cf = None
+        if capd is not None:
+            cf = capd[k][:, :1].expand(-1, fg.T_pad).contiguous()
+        out = eng.predict(fit, fg, seed=0, components=False, series_id=sid[k], interval_method=method, cap=cf)
+        return fit, out
+
+    run(0)
+    torch.cuda.synchronize()
+    eng.ctx.set_timing(True)
+    t0 = time.perf_counter()
+    stats = []
+    for k in range(len(chunks)):
+        fit, out = run(k)
+        stats.append((fit.n_eval.double().mean().item(), (fit.status == 70).double().mean().item()))
+        print(f"chunk {k + 1}/{len(chunks)}", file=sys.stderr, flush=True)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    kern = {}
+    for name, ms, _ in eng.ctx.read_timings():
+        kern[name] = kern.get(name, 0.0) + ms
+    eng.ctx.set_timing(False)
+    res = {"metric": "series fit+forecast/sec", "config_index": args.config, "value": n / el,
+           "unit": "series/s", "n_gpus": 1, "seconds": el, "workload": work, "chunk": chunk,
+           "kernels_ms_total": kern,
+           "n_eval_mean": float(np.mean([s[0] for s in stats])),
+           "map_certified": float(np.mean([s[1] for s in stats])),
+           "data": "synthetic (SURVEY.md §8d generators)"}
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
