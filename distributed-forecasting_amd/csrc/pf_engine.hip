@@ -73,6 +73,12 @@ __device__ unsigned long long pf_dbg[32];
 #define PF_COUNT(i) do { } while (0)
 #endif
 
+// diagnostic switch (environment): "1" enables
+static bool getenv_flag(const char *name) {
+  const char *v = getenv(name);
+  return v && v[0] == '1';
+}
+
 static int set_err(pf_ctx *ctx, const char *msg) {
   char *dst = ctx ? ctx->err : g_err_noctx;
   snprintf(dst, 512, "%s", msg);
@@ -486,7 +492,8 @@ struct FitSmem {
     return (size_t)ny + 64 * 4 + 2 * KMAX + 2 * NL + 2 * NW + 128 + NW + 128 + 4 + 2 +
            (size_t)NW * NSET * KMAX + 128 + 32 + 32 + 4 + 4 * 64;
   }
-  static __host__ __device__ size_t union_bytes(int P, bool polish) {
+  static __host__ __device__ size_t union_bytes(int P, int S, bool polish) {
+    (void)S;
     const size_t lbb = sizeof(LbLds<ModeTr<MODE>::PW>) + 16;
     if (!polish) return lbb;
     const size_t tiles = (size_t)10 * 4 * 64 * sizeof(double);
@@ -495,8 +502,8 @@ struct FitSmem {
     size_t u = lbb > tiles ? lbb : tiles;
     return u > hm ? u : hm;
   }
-  static __host__ __device__ size_t bytes(int ny, int P, bool polish) {
-    return fixed_doubles(ny) * sizeof(double) + union_bytes(P, polish) + 64;
+  static __host__ __device__ size_t bytes(int ny, int P, int S, bool polish) {
+    return fixed_doubles(ny) * sizeof(double) + union_bytes(P, S, polish) + 64;
   }
   __device__ void carve(char *base, int ny, int P) {
     double *p = reinterpret_cast<double *>(base);
@@ -1434,8 +1441,11 @@ __device__ __forceinline__ bool lbfgs_advance(const pf_fit_opts &o, LbLds<PW> &L
 #include "pf_polish.h"
 
 // ---------------------------------------------------------------- K3 kernel
+// pass 0: first L-BFGS run; pass > 0: resume the series the polish did not
+// certify.  o: this pass's options (iteration cap); warm: the cap is the
+// warm-up cap (MAXIT -> WARMUP).
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
-__device__ __forceinline__ void fit_body(const FitKArgs &a) {
+__device__ __forceinline__ void fit_body(const FitKArgs &a, int pass, const pf_fit_opts &o, bool warm) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   FitSmem<NW, KMAX, MODE> sm;
   sm.carve(smem_raw, a.TQ, a.P);
@@ -1443,7 +1453,7 @@ __device__ __forceinline__ void fit_body(const FitKArgs &a) {
   const int P = a.P;
   double *th_out = a.theta + (size_t)s * P;
   const int st_in = a.status[s];
-  if (a.pass > 0) {
+  if (pass > 0) {
     // resume pass: only series whose polish did not certify the MAP
     if (st_in == PF_ST_CONSTANT || st_in == PF_ST_BADINIT || st_in == PF_ST_MAP) return;
   } else if (st_in == PF_ST_CONSTANT) {
@@ -1497,7 +1507,7 @@ __device__ __forceinline__ void fit_body(const FitKArgs &a) {
       if (lane == 0) { L.z.fq = fq; L.z.n_eval = n_eval; }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
-      const bool need = lbfgs_advance(a.o, L, xq, gq, gpq, bad);
+      const bool need = lbfgs_advance(o, L, xq, gq, gpq, bad);
       if (need) publish_theta<NW, KMAX, MODE>(a, sm, xq);
       if (lane == 0) sm.flag[0] = need ? 1 : 0;
     }
@@ -1509,14 +1519,14 @@ __device__ __forceinline__ void fit_body(const FitKArgs &a) {
   const double f_stan = f;
   int st_stan = L.z.ret;
   const int it_stan = L.z.itNum;
-  if (a.warm_cap && st_stan == PF_ST_MAXIT) st_stan = PF_ST_WARMUP;
+  if (warm && st_stan == PF_ST_MAXIT) st_stan = PF_ST_WARMUP;
   if (threadIdx.x < 64) {
 #pragma unroll
     for (int h = 0; h < PW; ++h)
       if (lane + 64 * h < P) th_out[lane + 64 * h] = L.xk[lane + 64 * h];
     if (lane == 0) {
       a.f_out[s] = f;
-      if (a.pass == 0) {
+      if (pass == 0) {
         a.f_stan[s] = f_stan;
         a.n_iter[s] = it_stan;
         a.n_eval[s] = n_eval;
@@ -1571,11 +1581,11 @@ struct FitOcc {
 };
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
 __global__ __launch_bounds__(NW * 64, FitOcc<KMAX>::W) void k_fit(FitKArgs a) {
-  fit_body<NW, KMAX, O0, O1, O2, MODE>(a);
+  fit_body<NW, KMAX, O0, O1, O2, MODE>(a, a.pass, a.o, a.warm_cap != 0);
 }
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
 __global__ __launch_bounds__(NW * 64, FitOcc<KMAX>::W) void k_fit_resume(FitKArgs a) {
-  fit_body<NW, KMAX, O0, O1, O2, MODE>(a);
+  fit_body<NW, KMAX, O0, O1, O2, MODE>(a, a.pass, a.o, a.warm_cap != 0);
 }
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
 __global__ __launch_bounds__(NW * 64, 2) void k_polish(FitKArgs a) {
@@ -1584,6 +1594,27 @@ __global__ __launch_bounds__(NW * 64, 2) void k_polish(FitKArgs a) {
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
 __global__ __launch_bounds__(NW * 64, 2) void k_polish_resume(FitKArgs a) {
   polish_body<NW, KMAX, O0, O1, O2, MODE>(a);
+}
+// The warm-up hand-off of launch_fitlike — L-BFGS warm-up -> polish, once
+// more for uncertified series, then Stan's full rules -> polish — per series
+// in one launch: each series moves on to its polish as soon as its own
+// L-BFGS phase ends, so the batch's slow fits overlap other series' polish
+// instead of the two phases being separated by a grid-wide kernel boundary.
+template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
+__global__ __launch_bounds__(NW * 64, 2) void k_fit_polish(FitKArgs a) {
+  const int W = a.o.lbfgs_warmup;
+  for (int ps = 0; ps < 3; ++ps) {
+    const bool warm = ps < 2;
+    pf_fit_opts o = a.o;
+    o.max_iter = warm ? W : a.o.max_iter;
+    if (!warm) o.lbfgs_warmup_evals = 0;
+    fit_body<NW, KMAX, O0, O1, O2, MODE>(a, ps, o, warm);
+    __syncthreads();
+    polish_body<NW, KMAX, O0, O1, O2, MODE>(a);
+    __syncthreads();
+    const int st = __builtin_amdgcn_readfirstlane(__atomic_load_n(&a.status[blockIdx.x], __ATOMIC_RELAXED));
+    if (st == PF_ST_MAP || st == PF_ST_CONSTANT || st == PF_ST_BADINIT) break;
+  }
 }
 
 // ============================================================================
@@ -1969,8 +2000,8 @@ template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
 int launch_fitlike(pf_ctx *ctx, bool fit, const FitKArgs &a, int n, hipStream_t st) {
   // the polish handles K <= 32 and 2 + S <= 32 (J space of two 32-column blocks)
   constexpr bool HAS_POLISH = KMAX <= 32 && (MODE & PF_MODE_LOGI) == 0;
-  const size_t smem = FitSmem<NW, KMAX, MODE>::bytes(a.TQ, a.P, false);
-  const size_t smem_p = FitSmem<NW, KMAX, MODE>::bytes(a.TQ, a.P, HAS_POLISH);
+  const size_t smem = FitSmem<NW, KMAX, MODE>::bytes(a.TQ, a.P, a.S, false);
+  const size_t smem_p = FitSmem<NW, KMAX, MODE>::bytes(a.TQ, a.P, a.S, HAS_POLISH);
   if (smem > 160 * 1024) return set_err(ctx, "fit: series too long for the LDS budget");
   if (fit) {
     void (*kf[2])(FitKArgs) = {k_fit<NW, KMAX, O0, O1, O2, MODE>,
@@ -2002,6 +2033,17 @@ int launch_fitlike(pf_ctx *ctx, bool fit, const FitKArgs &a, int n, hipStream_t 
       npass = 3;
     } else {
       caps[0] = a.o.max_iter; warm[0] = 0;
+    }
+    if (npass == 3 && !getenv_flag("PF_SPLIT_POLISH")) {
+      if constexpr (HAS_POLISH) {
+        auto kfp = k_fit_polish<NW, KMAX, O0, O1, O2, MODE>;
+        PF_HIP(ctx, hipFuncSetAttribute((const void *)kfp, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)(smem_p > smem ? smem_p : smem)));
+        PF_TIMED_LAUNCH(ctx, "k_fit_polish", n, st, kfp, dim3(n), dim3(NW * 64),
+                        smem_p > smem ? smem_p : smem, st, a);
+        PF_HIP(ctx, hipGetLastError());
+        return 0;
+      }
     }
     for (int ps = 0; ps < npass; ++ps) {
       FitKArgs b = a;

@@ -440,7 +440,7 @@ def test_timing_records(eng):
     rec = eng.ctx.read_timings()
     eng.ctx.set_timing(False)
     names = [r[0] for r in rec]
-    for k in ("k_prepare", "k_fit", "k_polish", "k_predict_det", "k_predict_mc"):
+    for k in ("k_prepare", "k_fit_polish", "k_predict_det", "k_predict_mc"):
         assert k in names
     assert all(r[1] > 0 for r in rec)
 
