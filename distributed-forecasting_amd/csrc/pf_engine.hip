@@ -1600,17 +1600,28 @@ __global__ __launch_bounds__(NW * 64, 2) void k_polish_resume(FitKArgs a) {
 // in one launch: each series moves on to its polish as soon as its own
 // L-BFGS phase ends, so the batch's slow fits overlap other series' polish
 // instead of the two phases being separated by a grid-wide kernel boundary.
+// The two phases are separate (non-inlined) functions so each gets its own
+// register allocation: inlined together, the polish's pressure spilled
+// values of the L-BFGS evaluation loop.
+template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
+__device__ __noinline__ void fit_phase(const FitKArgs &a, int pass, int max_iter, bool warm) {
+  pf_fit_opts o = a.o;
+  o.max_iter = max_iter;
+  if (!warm) o.lbfgs_warmup_evals = 0;
+  fit_body<NW, KMAX, O0, O1, O2, MODE>(a, pass, o, warm);
+}
+template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
+__device__ __noinline__ void polish_phase(const FitKArgs &a) {
+  polish_body<NW, KMAX, O0, O1, O2, MODE>(a);
+}
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
 __global__ __launch_bounds__(NW * 64, 2) void k_fit_polish(FitKArgs a) {
   const int W = a.o.lbfgs_warmup;
   for (int ps = 0; ps < 3; ++ps) {
     const bool warm = ps < 2;
-    pf_fit_opts o = a.o;
-    o.max_iter = warm ? W : a.o.max_iter;
-    if (!warm) o.lbfgs_warmup_evals = 0;
-    fit_body<NW, KMAX, O0, O1, O2, MODE>(a, ps, o, warm);
+    fit_phase<NW, KMAX, O0, O1, O2, MODE>(a, ps, warm ? W : a.o.max_iter, warm);
     __syncthreads();
-    polish_body<NW, KMAX, O0, O1, O2, MODE>(a);
+    polish_phase<NW, KMAX, O0, O1, O2, MODE>(a);
     __syncthreads();
     const int st = __builtin_amdgcn_readfirstlane(__atomic_load_n(&a.status[blockIdx.x], __ATOMIC_RELAXED));
     if (st == PF_ST_MAP || st == PF_ST_CONSTANT || st == PF_ST_BADINIT) break;

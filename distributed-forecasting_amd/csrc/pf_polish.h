@@ -218,6 +218,15 @@ __device__ __forceinline__ void hessian_collective(const FitKArgs &a, FitSmem<NW
   }
 }
 
+// The matrix stride re-materialised inside a loop body: keeps the compiler
+// from hoisting one LDS address per matrix row out of the QP loops (16+ live
+// VGPRs that end up spilled to scratch and reloaded on every row access).
+__device__ __forceinline__ int pf_opaque(int v) {
+  int r;
+  asm volatile("s_mov_b32 %0, %1" : "=s"(r) : "s"(__builtin_amdgcn_readfirstlane(v)));
+  return r;
+}
+
 // Symmetric sweep operator on A (P x P, stride LD, LDS; wave-local, lane =
 // column j).  Sweeping k in (rev = false) or out (rev = true) with pivot
 // d = A[k][k]:  A[i][j] -= A[i][k] A[k][j] / d  (i, j != k),
@@ -225,8 +234,9 @@ __device__ __forceinline__ void hessian_collective(const FitKArgs &a, FitSmem<NW
 // After sweeping the set F, A_FF = -(H_FF)^-1, A_FZ = (H_FF)^-1 H_FZ and
 // A_ZZ is the Schur complement, so each active-set change costs one O(P^2)
 // sweep instead of a refactorisation.  A sweep-in needs d > 0 (H_FF PD).
-__device__ __forceinline__ bool wave_sweep(double *A, int LD, int P, int k, bool rev) {
+__device__ __forceinline__ bool wave_sweep(double *A, int LD_, int P, int k, bool rev) {
   const int j = pf_lane();
+  const int LD = pf_opaque(LD_);
   const double d = A[k * LD + k];
   if (!rev && !(d > 0.0)) return false;
   if (rev && !(d < 0.0)) return false;
@@ -292,28 +302,30 @@ __device__ __forceinline__ void sweep_in_free(const FitKArgs &a, FitSmem<NW, KMA
   while (fm) {
     const int k = __ffsll((long long)fm) - 1;
     fm &= fm - 1;
-    const double d = A[k * LD + k];
+    const int LDl = pf_opaque(LD);
+    const double d = A[k * LDl + k];
     if (!(d > 0.0)) {  // uniform across the workgroup
       if (threadIdx.x == 0) sm.flag[1] = 1;
       break;
     }
     const double inv = 1.0 / d;
-    const double akj = (lane < P) ? A[k * LD + lane] : 0.0;
+    const double akj = (lane < P) ? A[k * LDl + lane] : 0.0;
     const double sj = akj * inv;
     if (lane < P) {
+      double *Ar = A + r0 * LDl + lane;
 #pragma unroll
       for (int q = 0; q < RW; ++q) {
         const int i = r0 + q;
-        if (i < P && i != k) A[i * LD + lane] = fma(-readlane_f64(akj, i), sj, A[i * LD + lane]);
+        if (i < P && i != k) Ar[q * LDl] = fma(-readlane_f64(akj, i), sj, Ar[q * LDl]);
       }
     }
     __syncthreads();
     if (wave == 0) {
       if (lane < P && lane != k) {
-        A[k * LD + lane] = sj;
-        A[lane * LD + k] = sj;
+        A[k * LDl + lane] = sj;
+        A[lane * LDl + k] = sj;
       }
-      if (lane == k) A[k * LD + k] = -inv;
+      if (lane == k) A[k * LDl + k] = -inv;
     }
     __syncthreads();
     PF_COUNT(26);
@@ -323,8 +335,9 @@ __device__ __forceinline__ void sweep_in_free(const FitKArgs &a, FitSmem<NW, KMA
 
 // u = A v for the symmetric swept matrix (lane p: u_p = sum_q A[q][p] v_q;
 // v staged in LDS, read by uniform broadcast)
-__device__ __forceinline__ double wave_symv(const double *A, int LD, int P, const double *v) {
+__device__ __forceinline__ double wave_symv(const double *A, int LD_, int P, const double *v) {
   const int p = pf_lane();
+  const int LD = pf_opaque(LD_);
   double u0 = 0.0, u1 = 0.0;
   if (p < P) {
     int q = 0;
