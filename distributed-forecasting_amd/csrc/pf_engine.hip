@@ -498,7 +498,9 @@ struct FitSmem {
     if (!polish) return lbb;
     const size_t tiles = (size_t)10 * 4 * 64 * sizeof(double);
     const int LD = P | 1;
-    const size_t hm = 2 * (size_t)P * LD * sizeof(double);
+    // H, A + 8 padding rows (80.7 KB with the fixed part at P = 54, T = 1826:
+    // two workgroups per CU)
+    const size_t hm = (2 * (size_t)P + 8) * LD * sizeof(double);
     size_t u = lbb > tiles ? lbb : tiles;
     return u > hm ? u : hm;
   }

@@ -42,7 +42,9 @@ template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
 __device__ __forceinline__ void hessian_collective(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, double x,
                                    double gh, double *ws) {
   const int lane = pf_lane(), wave = pf_wave();
-  const int S = a.S, K = a.K, T = a.T, Tp = a.Tp, P = a.P;
+  const int S = __builtin_amdgcn_readfirstlane(a.S), K = __builtin_amdgcn_readfirstlane(a.K);
+  const int T = __builtin_amdgcn_readfirstlane(a.T), Tp = __builtin_amdgcn_readfirstlane(a.Tp);
+  const int P = __builtin_amdgcn_readfirstlane(a.P);
   {
     PV<1> xv;
     xv[0] = x;
@@ -234,9 +236,10 @@ __device__ __forceinline__ int pf_opaque(int v) {
 // After sweeping the set F, A_FF = -(H_FF)^-1, A_FZ = (H_FF)^-1 H_FZ and
 // A_ZZ is the Schur complement, so each active-set change costs one O(P^2)
 // sweep instead of a refactorisation.  A sweep-in needs d > 0 (H_FF PD).
-__device__ __forceinline__ bool wave_sweep(double *A, int LD_, int P, int k, bool rev) {
+__device__ __forceinline__ bool wave_sweep(double *A, int LD_, int P_, int k_, bool rev) {
   const int j = pf_lane();
   const int LD = pf_opaque(LD_);
+  const int P = __builtin_amdgcn_readfirstlane(P_), k = __builtin_amdgcn_readfirstlane(k_);
   const double d = A[k * LD + k];
   if (!rev && !(d > 0.0)) return false;
   if (rev && !(d < 0.0)) return false;
@@ -244,24 +247,20 @@ __device__ __forceinline__ bool wave_sweep(double *A, int LD_, int P, int k, boo
   const double akj = (j < P) ? A[k * LD + j] : 0.0;
   const double sj = akj * inv;
   // row k (= column k) is held across lanes in akj: A[k][i] = readlane(akj, i).
-  // Rows in blocks of 8, all loads of a block before its stores; every
-  // per-row condition is uniform (lane k's own column is rewritten below).
+  // Rows in blocks of 8, all loads of a block before its stores, no per-row
+  // conditions: A carries 8 padding rows past P (their values are don't-care)
+  // and row / column k are rewritten below.
   if (j < P) {
+    double *Aj = A + j;
     for (int i0 = 0; i0 < P; i0 += 8) {
       double av[8], ak[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        const int i = i0 + q;
-        if (i < P) {
-          ak[q] = readlane_f64(akj, i);
-          av[q] = A[i * LD + j];
-        }
+        ak[q] = readlane_f64(akj, (i0 + q) & 63);
+        av[q] = Aj[(i0 + q) * LD];
       }
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int i = i0 + q;
-        if (i < P && i != k) A[i * LD + j] = fma(-ak[q], sj, av[q]);
-      }
+      for (int q = 0; q < 8; ++q) Aj[(i0 + q) * LD] = fma(-ak[q], sj, av[q]);
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -287,13 +286,18 @@ template <int NW, int KMAX, int MODE>
 __device__ __forceinline__ void sweep_in_free(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, double gh,
                                               double c) {
   const int lane = pf_lane(), wave = pf_wave();
-  const int P = a.P, S = a.S, LD = sm.LD;
+  const int P = __builtin_amdgcn_readfirstlane(a.P), S = __builtin_amdgcn_readfirstlane(a.S);
+  const int LD = __builtin_amdgcn_readfirstlane(sm.LD);
   const double *H = sm.U;
   double *A = sm.U + (size_t)P * LD;
   constexpr int RW = (64 + NW - 1) / NW;  // rows per wave
   const int r0 = wave * RW;
   if (lane < P)
     for (int i = r0; i < r0 + RW && i < P; ++i) A[i * LD + lane] = H[i * LD + lane];
+  // 8 zeroed padding rows past P (read unconditionally by the batched
+  // sweep / symv loops)
+  if (lane < LD)
+    for (int i = P + wave; i < P + 8; i += NW) A[i * LD + lane] = 0.0;
   if (threadIdx.x == 0) sm.flag[1] = 0;
   __syncthreads();
   const bool isd = (lane >= 2 && lane < 2 + S);
@@ -335,19 +339,27 @@ __device__ __forceinline__ void sweep_in_free(const FitKArgs &a, FitSmem<NW, KMA
 
 // u = A v for the symmetric swept matrix (lane p: u_p = sum_q A[q][p] v_q;
 // v staged in LDS, read by uniform broadcast)
-__device__ __forceinline__ double wave_symv(const double *A, int LD_, int P, const double *v) {
+__device__ __forceinline__ double wave_symv(const double *A, int LD_, int P_, const double *v) {
   const int p = pf_lane();
   const int LD = pf_opaque(LD_);
-  double u0 = 0.0, u1 = 0.0;
+  const int P = __builtin_amdgcn_readfirstlane(P_);
+  double u[4] = {0.0, 0.0, 0.0, 0.0};
   if (p < P) {
-    int q = 0;
-    for (; q + 1 < P; q += 2) {
-      u0 = fma(A[q * LD + p], v[q], u0);
-      u1 = fma(A[(q + 1) * LD + p], v[q + 1], u1);
+    // 8 rows per batch, all loads issued before the FMAs (one LDS latency
+    // per batch); rows past P read the zeroed padding rows with v = 0
+    const double *Ap = A + p;
+    for (int q0 = 0; q0 < P; q0 += 8) {
+      double av[8], vv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        av[j] = Ap[(q0 + j) * LD];
+        vv[j] = v[q0 + j];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) u[j & 3] = fma(av[j], vv[j], u[j & 3]);
     }
-    if (q < P) u0 = fma(A[q * LD + p], v[q], u0);
   }
-  return u0 + u1;
+  return (u[0] + u[1]) + (u[2] + u[3]);
 }
 
 // Active-set solution of min gh.(z-x) + (z-x)'H(z-x)/2 + c||z_delta||_1 (wave 0).
@@ -362,7 +374,8 @@ template <int NW, int KMAX, int MODE>
 __device__ __forceinline__ bool qp_active(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm, double x, double gh, double c,
                           double &z, int &nsolve, bool &zero, double &sgn_, bool warm) {
   const int lane = pf_lane();
-  const int P = a.P, S = a.S, LD = sm.LD;
+  const int P = __builtin_amdgcn_readfirstlane(a.P), S = __builtin_amdgcn_readfirstlane(a.S);
+  const int LD = __builtin_amdgcn_readfirstlane(sm.LD);
   double *A = sm.U + (size_t)P * LD;
   const bool isd = (lane >= 2 && lane < 2 + S);
   if (isd) {
