@@ -14,10 +14,12 @@ from .batch import FittedBatch, bucket_groups, series_id, shard_of  # noqa: F401
 from .forecaster import Prophet, SIMPLE_ATTRIBUTES  # noqa: F401
 from .training import (train_model, make_prediction, forecast_item,  # noqa: F401
                        forecast_store_item, forecast_store_items, forecast_items,
-                       extract_params, reference_model)
+                       extract_params, reference_model, allocate_forecasts,
+                       forecast_partitions)
 from .serving import ParamsStore, ForecastStoreItemModel, predict_udf, register_model  # noqa: F401
 from .diagnostics import cv_metrics_batch, cv_metrics_device, generate_cutoffs  # noqa: F401
 from .engine import future_dates  # noqa: F401
+from .holidays import HolidaySpec, holiday_spec  # noqa: F401
 
 __all__ = ["Engine", "ProphetConfig", "FitResult", "DeviceGrid", "build_grid", "future_dates",
            "pad_rows", "EngineUnavailable", "STATUS_NAMES", "CV_METRICS", "FittedBatch",
@@ -25,4 +27,5 @@ __all__ = ["Engine", "ProphetConfig", "FitResult", "DeviceGrid", "build_grid", "
            "train_model", "make_prediction", "forecast_item", "forecast_store_item",
            "forecast_store_items", "forecast_items", "extract_params", "reference_model",
            "ParamsStore", "ForecastStoreItemModel", "predict_udf", "register_model",
-           "cv_metrics_batch", "cv_metrics_device", "generate_cutoffs"]
+           "cv_metrics_batch", "cv_metrics_device", "generate_cutoffs", "allocate_forecasts",
+           "forecast_partitions", "HolidaySpec", "holiday_spec"]

@@ -184,3 +184,39 @@ def forecast_store_items(df: pd.DataFrame, keys=("store", "item"), *, periods: i
 def forecast_items(df: pd.DataFrame, **kw):
     """Batched ``groupBy('item').applyInPandas(forecast_item, ...)`` (:232-233)."""
     return forecast_store_items(df, keys=("item",), **kw)
+
+
+def allocate_forecasts(item_forecast: pd.DataFrame, sales: pd.DataFrame,
+                       training_date=None) -> pd.DataFrame:
+    """The item-level stage's allocation (02_training.py:235-247): store
+    ratios ``sales / SUM(sales) OVER (PARTITION BY item)`` over the raw
+    (store, item, sales) table, joined on item; ``y`` and ``yhat`` scaled by
+    the ratio.  Columns ``date, store, item, sales, forecast, training_date``
+    — the ``allocated_forecasts`` table the fine-grained stage reads back
+    (with NaN ``sales`` on the 90 future rows)."""
+    val = "sales" if "sales" in sales else "y"
+    tot = sales.groupby(["store", "item"], as_index=False)[val].sum()
+    tot["ratio"] = tot[val] / tot.groupby("item")[val].transform("sum")
+    res = item_forecast.merge(tot[["store", "item", "ratio"]], on="item")
+    out = pd.DataFrame({
+        "date": res["ds"],
+        "store": res["store"].astype(np.int32),
+        "item": res["item"].astype(np.int32),
+        "sales": (res["y"] * res["ratio"]).astype(np.float32),
+        "forecast": (res["yhat"] * res["ratio"]).astype(np.float32),
+    })
+    out["training_date"] = pd.Timestamp.today().normalize() if training_date is None else training_date
+    return out
+
+
+def forecast_partitions(keys=("store", "item"), **kw):
+    """A ``mapInPandas``-compatible function: every group frame of a Spark
+    partition (an iterator of pandas frames holding whole groups, e.g. after
+    ``repartition('store', 'item')``) goes to the GPU in one batched call
+    instead of one Python call per group; yields the same rows and schema as
+    ``applyInPandas(forecast_store_item, ...)``."""
+    def run(frames):
+        parts = [f for f in frames if len(f)]
+        if parts:
+            yield forecast_store_items(pd.concat(parts, ignore_index=True), keys=keys, **kw)
+    return run

@@ -475,3 +475,26 @@ def test_future_intervals_vs_oracle_sampler(eng, horizon):
         yh = out["yhat"][s, :fg.T].cpu().numpy()
         assert np.all(out["yhat_lower"][s, :fg.T].cpu().numpy() <= yh + 1e-3 * abs(yh).max())
         assert np.all(out["yhat_upper"][s, :fg.T].cpu().numpy() >= yh - 1e-3 * abs(yh).max())
+
+
+def test_partition_adapter_and_allocated_second_stage(eng):
+    """forecast_partitions (mapInPandas shape) returns the rows of the
+    per-group applyInPandas call; the item-level stage's allocated table
+    (90 NaN future rows per series) fed back as history
+    gives the 2006-row fine-grained forecasts."""
+    import pandas as pd
+    df = synthetic.store_item_frame(2, 2, "2016-01-01", "2017-12-31")
+    parts = [df[df.store == s] for s in (1, 2)]
+    got = pd.concat(list(dfa.forecast_partitions()(iter(parts))), ignore_index=True)
+    ref = dfa.forecast_store_items(df)
+    key = ["store", "item", "ds"]
+    got, ref = got.sort_values(key).reset_index(drop=True), ref.sort_values(key).reset_index(drop=True)
+    assert got.equals(ref)
+    items = df.groupby(["item", "ds"], as_index=False)["y"].sum()
+    fi = dfa.forecast_items(items)
+    alloc = dfa.allocate_forecasts(fi, df.rename(columns={"y": "sales"}))
+    hist = alloc.rename(columns={"date": "ds", "sales": "y"})[["ds", "store", "item", "y"]]
+    fine = dfa.forecast_store_items(hist)
+    T = len(df.ds.unique())
+    assert len(fine) == 4 * (T + 90 + 90)
+    assert fine.groupby(["store", "item"]).size().eq(T + 180).all()

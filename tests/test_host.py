@@ -88,6 +88,22 @@ def test_holiday_spec_errors():
         H.holiday_spec(hd.drop(columns="prior_scale").assign(lower_window=0))
 
 
+def test_allocate_forecasts():
+    """02_training.py:235-247: ratios sales / SUM(sales) OVER (PARTITION BY
+    item); y and yhat scaled; NaN future y stays NaN."""
+    import pandas as pd
+    sales = pd.DataFrame({"store": [1, 2, 1, 2], "item": [7, 7, 8, 8], "sales": [30.0, 10.0, 5.0, 5.0]})
+    fc = pd.DataFrame({"ds": pd.to_datetime(["2018-01-01", "2018-01-02"] * 2), "item": [7, 7, 8, 8],
+                       "y": [4.0, np.nan, 2.0, np.nan], "yhat": [8.0, 8.0, 2.0, 4.0]})
+    out = dfa.allocate_forecasts(fc, sales, training_date=pd.Timestamp("2020-01-01"))
+    assert list(out.columns) == ["date", "store", "item", "sales", "forecast", "training_date"]
+    r = out[(out.store == 1) & (out.item == 7)].sort_values("date")
+    assert np.allclose(r["forecast"], [6.0, 6.0]) and r["sales"].iloc[0] == 3.0 and np.isnan(r["sales"].iloc[1])
+    r = out[(out.store == 2) & (out.item == 8)].sort_values("date")
+    assert np.allclose(r["forecast"], [1.0, 2.0])
+    assert len(out) == 8
+
+
 def test_seasonality_auto_rules():
     cfg = ProphetConfig()
     d = NS_PER_DAY
