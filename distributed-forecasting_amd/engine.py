@@ -167,6 +167,20 @@ class DeviceGrid:
         return o
 
 
+def _device_dates(ds_ns: np.ndarray, dev) -> torch.Tensor:
+    """Grid dates on the device.  A regular grid (every daily / hourly bucket
+    in practice) is generated there (start + k * step: an asynchronous device
+    op), so building a grid never waits on a pageable host-to-device copy —
+    which is stream-ordered and would stall the host until the GPU drained the
+    previous batch's kernels."""
+    T = ds_ns.shape[0]
+    if T >= 2:
+        step = int(ds_ns[1] - ds_ns[0])
+        if step > 0 and int(ds_ns[-1] - ds_ns[0]) == step * (T - 1) and np.all(np.diff(ds_ns) == step):
+            return torch.arange(T, dtype=torch.int64, device=dev) * step + int(ds_ns[0])
+    return torch.from_numpy(ds_ns).to(dev)
+
+
 def build_grid(ds_ns: np.ndarray, seasons, *, start_ns: int, t_scale_ns: int,
                n_changepoints: int = 25, changepoint_range: float = 0.8,
                t_change: torch.Tensor | None = None, device: int = 0,
@@ -185,7 +199,7 @@ def build_grid(ds_ns: np.ndarray, seasons, *, start_ns: int, t_scale_ns: int,
     if K == 0:
         raise ValueError("no seasonality columns: the zero-feature dummy X is not supported yet")
     dev = torch.device("cuda", device)
-    ds_d = torch.from_numpy(ds_ns).to(dev)
+    ds_d = _device_dates(ds_ns, dev)
     t = torch.empty(Tp, dtype=torch.float64, device=dev)
     XT = torch.empty(K * Tp, dtype=torch.float64, device=dev)
     seg = torch.empty(Tp, dtype=torch.int32, device=dev)

@@ -54,15 +54,16 @@ def main(src, tag):
             d["frac_active_inst_any"] = d.get("SQ_ACTIVE_INST_ANY", 0) / w
     with open(os.path.join(prof, f"{tag}_pmc.json"), "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
-    if "k_fit" in out and "hbm_bytes_per_launch" in out["k_fit"]:
+    kf = "k_fit_polish" if "k_fit_polish" in out else "k_fit"
+    if kf in out and "hbm_bytes_per_launch" in out[kf]:
         with open(os.path.join(prof, "pmc_k_fit.json"), "w") as f:
-            json.dump({"tag": tag, "kernel": "k_fit",
-                       "hbm_bytes_per_launch": out["k_fit"]["hbm_bytes_per_launch"],
-                       "FETCH_SIZE_KiB": out["k_fit"]["FETCH_SIZE"],
-                       "WRITE_SIZE_KiB": out["k_fit"]["WRITE_SIZE"],
+            json.dump({"tag": tag, "kernel": kf,
+                       "hbm_bytes_per_launch": out[kf]["hbm_bytes_per_launch"],
+                       "FETCH_SIZE_KiB": out[kf]["FETCH_SIZE"],
+                       "WRITE_SIZE_KiB": out[kf]["WRITE_SIZE"],
                        "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE half-count)"},
                       f, indent=1)
-    for k in ("k_fit", "k_polish", "k_predict_det", "k_predict_mc"):
+    for k in ("k_fit", "k_fit_polish", "k_polish", "k_predict_det", "k_predict_mc"):
         if k in out:
             print(k, {a: (round(b, 4) if isinstance(b, float) else b) for a, b in out[k].items()})
 
