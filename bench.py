@@ -253,10 +253,17 @@ def main():
     E_all = np.array(man["E"], dtype=np.float64)
     E_mean = float(E_all.mean())
     evals = float(fit.n_eval.double().sum().item())
-    flops = evals * FLOPS_PER_EVAL
     fit_kernel = "k_fit_polish" if "k_fit_polish" in kern_avg else "k_fit"
     fit_s = kern_avg.get(fit_kernel, float("nan")) / 1e3
-    achieved = flops / fit_s / 1e12
+    # algorithmic work per series = E x 4T(F+2C), E = the
+    # oracle's Stan-faithful evaluation count for that series (fixed per
+    # series, tests/golden/bench_manifest.json) -- the Stan fit the launch
+    # replaces; the engine performs fewer evaluations (warm-up + polish)
+    mine_E = E_all[mine] if len(E_all) >= len(keys) else np.full(n, E_mean)
+    flops_alg = float(mine_E.sum()) * FLOPS_PER_EVAL
+    flops = evals * FLOPS_PER_EVAL
+    achieved = flops_alg / fit_s / 1e12
+    achieved_perf = flops / fit_s / 1e12
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_k_fit.json")
     if os.path.exists(pmc_path):
@@ -264,11 +271,16 @@ def main():
             traffic = json.load(f).get("hbm_bytes_per_launch")
     roof = {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
             "frac": achieved / PEAK_FP64_TFLOPS, "traffic": traffic, "kernel": fit_kernel,
-            "kernel_ms": kern_avg.get(fit_kernel), "flops_per_launch": flops,
-            "evals_per_launch": evals,
-            "note": "FP64 compute-bound (MI355X FP64 vector peak = FP64 matrix peak = 78.6 TF); "
-                    "FLOPs = evaluations performed (n_eval) x 4T(F+2C); traffic = HBM bytes per "
-                    "launch from rocprofv3 PMC (profiles/pmc_k_fit.json)"}
+            "kernel_ms": kern_avg.get(fit_kernel), "flops_per_launch": flops_alg,
+            "evals_algorithmic_per_launch": float(mine_E.sum()),
+            "evals_performed_per_launch": evals,
+            "achieved_performed": achieved_perf, "frac_performed": achieved_perf / PEAK_FP64_TFLOPS,
+            "note": "FP64 (MI355X FP64 vector peak = FP64 matrix peak = 78.6 TF).  achieved = SURVEY "
+                    "§8d algorithmic FLOPs (the oracle Stan run's evaluations E per series x "
+                    "4T(F+2C)) / the fused fit+polish kernel's time; achieved_performed counts only "
+                    "the L-BFGS evaluations the engine performed (its exact-MAP polish replaces "
+                    "Stan's remaining ~260 evaluations/series); traffic = HBM bytes per launch "
+                    "from rocprofv3 PMC (profiles/pmc_k_fit.json)"}
     # forecast kernel: HBM roofline of its algorithmic output bytes
     pred_bytes = 16.0 * len(fut) * n                # yhat, lo, hi, trend fp32 per row
     pred_s = (kern_avg.get("k_predict_det", float("nan")) +
