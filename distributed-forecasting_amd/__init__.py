@@ -20,6 +20,8 @@ from .serving import ParamsStore, ForecastStoreItemModel, predict_udf, register_
 from .diagnostics import cv_metrics_batch, cv_metrics_device, generate_cutoffs  # noqa: F401
 from .engine import future_dates  # noqa: F401
 from .holidays import HolidaySpec, holiday_spec  # noqa: F401
+from . import tuning  # noqa: F401
+from .tuning import hyperparameter_search, sample_trials  # noqa: F401
 
 __all__ = ["Engine", "ProphetConfig", "FitResult", "DeviceGrid", "build_grid", "future_dates",
            "pad_rows", "EngineUnavailable", "STATUS_NAMES", "CV_METRICS", "FittedBatch",
@@ -28,4 +30,5 @@ __all__ = ["Engine", "ProphetConfig", "FitResult", "DeviceGrid", "build_grid", "
            "forecast_store_items", "forecast_items", "extract_params", "reference_model",
            "ParamsStore", "ForecastStoreItemModel", "predict_udf", "register_model",
            "cv_metrics_batch", "cv_metrics_device", "generate_cutoffs", "allocate_forecasts",
-           "forecast_partitions", "HolidaySpec", "holiday_spec"]
+           "forecast_partitions", "HolidaySpec", "holiday_spec", "tuning",
+           "hyperparameter_search", "sample_trials"]

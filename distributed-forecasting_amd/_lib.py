@@ -48,7 +48,8 @@ class PfProblem(ctypes.Structure):
     _fields_ = [("n_series", i32), ("growth", i32), ("tau", ctypes.c_double),
                 ("grid", PfGrid),
                 ("sigmas", vp), ("s_a", vp), ("s_m", vp), ("y_scaled", vp), ("cap_scaled", vp),
-                ("fourier_orders", i32 * 3), ("season_mode", i32)]
+                ("fourier_orders", i32 * 3), ("season_mode", i32),
+                ("tau_series", vp), ("sigmas_series", vp)]
 
 
 class PfFitOpts(ctypes.Structure):

@@ -182,12 +182,13 @@ class FittedBatch:
     @classmethod
     def fit_dense(cls, engine: E.Engine, fit_ds: np.ndarray, Y, history_dates=None,
                   series_ids=None, polish: bool = True, seasons=None, cap=None,
-                  holidays=None) -> "FittedBatch":
+                  holidays=None, priors=None) -> "FittedBatch":
         """Fit every row of Y ([n, T] numpy or device tensor, raw y) on the
         sorted date grid ``fit_ds`` (K1 grid + K2/K3 fit).  ``seasons``
         overrides the auto rules (CV folds reuse the parent's seasonalities,
         UPSTREAM diagnostics.prophet_copy); ``holidays`` (holidays.HolidaySpec)
-        appends its indicator columns."""
+        appends its indicator columns.  ``priors``: per-row prior scales,
+        a dict of Engine.series_priors keyword arguments."""
         cfg = engine.config
         fit_ds = np.asarray(fit_ds, np.int64)
         T = fit_ds.shape[0]
@@ -214,7 +215,8 @@ class FittedBatch:
             if cap is None:
                 raise ValueError('Capacities must be supplied for logistic growth in column "cap"')
             capd = _dense(cap, n, T, grid.T_pad, dev)
-        fit = engine.fit(grid, Yd, polish=polish, cap=capd)
+        pri = engine.series_priors(grid, n, **priors) if priors is not None else None
+        fit = engine.fit(grid, Yd, polish=polish, cap=capd, priors=pri)
         hd = fit_ds if history_dates is None else history_dates
         return cls(engine, fit, np.unique(hd), fit_ds, series_ids)
 

@@ -344,6 +344,9 @@ struct FitKArgs {
   const int32_t *sgP;        // [TQ] seg | (#changepoints first active at this row) << 16
   const double *sigmas, *s_a, *s_m;
   double tau;
+  // hyperparameter batching: per-series prior scales (NULL: the shared
+  // tau / sigmas[K] above); sigmas_series is [n][K]
+  const double *tau_series, *sigmas_series;
   const double *y_scaled;
   const double *cap_scaled;  // [n][Tp] logistic capacity / y_scale (natural rows), else NULL
   double *ws;  // polish workspace [n][3][Tp]
@@ -478,7 +481,7 @@ struct FitSmem {
   double *rrw;      // [NW]
   double *gout;     // [128]
   double *fout;     // [4]
-  double *sig;      // [2] sigma, 1/sigma^2 of the published point
+  double *sig;      // [4] sigma, 1/sigma^2 of the published point; [2] = this series' tau
   double *gpart;    // [NW][NSET*KMAX] per-wave beta-gradient totals
   double *pd, *pz;  // [64] polish direction / scratch
   int *cpl;         // [64] per changepoint: owner thread
@@ -489,7 +492,7 @@ struct FitSmem {
   LbLds<ModeTr<MODE>::PW> *lb; // U view (Stan phase)
   int LD;           // stride of H / M in U (polish)
   static __host__ __device__ size_t fixed_doubles(int ny) {
-    return (size_t)ny + 64 * 4 + 2 * KMAX + 2 * NL + 2 * NW + 128 + NW + 128 + 4 + 2 +
+    return (size_t)ny + 64 * 4 + 2 * KMAX + 2 * NL + 2 * NW + 128 + NW + 128 + 4 + 4 +
            (size_t)NW * NSET * KMAX + 128 + 32 + 32 + 4 + 4 * 64;
   }
   static __host__ __device__ size_t union_bytes(int P, int S, bool polish) {
@@ -524,7 +527,7 @@ struct FitSmem {
     rrw = p; p += NW;
     gout = p; p += 128;
     fout = p; p += 4;
-    sig = p; p += 2;
+    sig = p; p += 4;
     gpart = p; p += (size_t)NW * NSET * KMAX;
     pd = p; p += 64;
     pz = p; p += 64;
@@ -617,7 +620,9 @@ __device__ __forceinline__ void load_consts(const FitKArgs &a, FitSmem<NW, KMAX,
   const int i = threadIdx.x;
   if (i < 64) {
     sm.ctc[i] = (i < a.S) ? a.t_change[i] : 0.0;
-    sm.csg[i] = (i < a.K) ? a.sigmas[i] : 1.0;
+    const double *sg = a.sigmas_series ? a.sigmas_series + (size_t)blockIdx.x * a.K : a.sigmas;
+    sm.csg[i] = (i < a.K) ? sg[i] : 1.0;
+    if (i == 0) sm.sig[2] = a.tau_series ? a.tau_series[blockIdx.x] : a.tau;
     sm.csm[i] = (i < a.K) ? a.s_m[i] : 0.0;
     sm.csa[i] = (i < a.K) ? a.s_a[i] : 0.0;
   }
@@ -792,7 +797,7 @@ __device__ __forceinline__ bool eval_assemble(const FitKArgs &a, FitSmem<NW, KMA
     tot0 += sm.wt0[w2];
     tot1 += sm.wt1[w2];
   }
-  const double sigma = sm.sig[0], inv_s2 = sm.sig[1];
+  const double sigma = sm.sig[0], inv_s2 = sm.sig[1], tau = sm.sig[2];
   const double ls = x;  // meaningful in lane 2+S only
   double gv = 0.0, fterm = 0.0;
   const int p = lane;
@@ -856,8 +861,8 @@ __device__ __forceinline__ bool eval_assemble(const FitKArgs &a, FitSmem<NW, KMA
   } else if (p < 2 + S && logistic) {
     const double d = x;
     const double sg = (d > 0.0) - (d < 0.0);
-    gv = -inv_s2 * gdL + sg / a.tau;
-    fterm = fabs(d) / a.tau;
+    gv = -inv_s2 * gdL + sg / tau;
+    fterm = fabs(d) / tau;
   } else if (p < 2 + S) {
     // suffix sums from changepoint j's first row: owner thread's inclusive
     // within-wave suffix + later waves - the owner's sum before that row
@@ -873,8 +878,8 @@ __device__ __forceinline__ bool eval_assemble(const FitKArgs &a, FitSmem<NW, KMA
     const double gdel = su1 - sm.ctc[j] * su0;
     const double d = x;
     const double sg = (d > 0.0) - (d < 0.0);
-    gv = (linear ? -inv_s2 * gdel : 0.0) + sg / a.tau;
-    fterm = fabs(d) / a.tau;
+    gv = (linear ? -inv_s2 * gdel : 0.0) + sg / tau;
+    fterm = fabs(d) / tau;
   } else if (p == 2 + S) {
     gv = (double)T - inv_s2 * rrt + 4.0 * sigma * sigma;
     fterm = 2.0 * sigma * sigma + (double)T * ls;
@@ -2004,6 +2009,8 @@ FitKArgs make_fit_args(const pf_problem *pb) {
   a.s_a = pb->s_a;
   a.s_m = pb->s_m;
   a.tau = pb->tau;
+  a.tau_series = pb->tau_series;
+  a.sigmas_series = pb->sigmas_series;
   a.y_scaled = pb->y_scaled;
   a.cap_scaled = pb->cap_scaled;
   return a;

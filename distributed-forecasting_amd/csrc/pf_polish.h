@@ -202,7 +202,7 @@ __device__ __forceinline__ void hessian_collective(const FitKArgs &a, FitSmem<NW
       double prior1 = 0.0, prior2 = 0.0;
       if (p == 0 || p == 1) { prior1 = x / 25.0; prior2 = 1.0 / 25.0; }
       else if (p > il) {
-        const double sg2 = a.sigmas[p - il - 1];
+        const double sg2 = sm.csg[p - il - 1];
         prior1 = x / (sg2 * sg2);
         prior2 = 1.0 / (sg2 * sg2);
       }
@@ -468,7 +468,7 @@ __device__ __forceinline__ bool polish_run(const FitKArgs &a, FitSmem<NW, KMAX, 
                            double &g, int &n_eval, int &n_newton) {
   const int lane = pf_lane(), wave = pf_wave();
   const int S = a.S;
-  const double c = 1.0 / a.tau;
+  const double c = 1.0 / sm.sig[2];
   const bool isd = (lane >= 2 && lane < 2 + S);
   double *ws = a.ws + (size_t)blockIdx.x * 3 * a.Tp;
   n_newton = 0;

@@ -48,7 +48,7 @@ def generate_cutoffs(ds_ns, horizon_ns: int, initial_ns: int, period_ns: int) ->
 def cv_metrics_device(engine: E.Engine, fit_ds: np.ndarray, Y, *, horizon_days: float = 90,
                       period_days: float = 360, initial_days: float = 730,
                       rolling_window: float = 0.1, seasons=None, coverage: bool = False,
-                      seed: int = 0, series_ids=None) -> torch.Tensor:
+                      seed: int = 0, series_ids=None, priors=None) -> torch.Tensor:
     """[n, 6] float64 device tensor: mse, rmse, mae, mape, smape, coverage
     (each the mean over horizons of the rolled metric) for every row of Y."""
     fit_ds = np.asarray(fit_ds, np.int64)
@@ -70,7 +70,7 @@ def cv_metrics_device(engine: E.Engine, fit_ds: np.ndarray, Y, *, horizon_days: 
         te = np.flatnonzero((fit_ds > c) & (fit_ds <= c + horizon))
         Ttr = int(tr.sum())
         fb = B.FittedBatch.fit_dense(engine, fit_ds[:Ttr], Yt[:, :Ttr], series_ids=series_ids,
-                                     seasons=seasons)
+                                     seasons=seasons, priors=priors)
         Tf, out = fb.predict(fit_ds[te], seed=seed,
                              n_samples=None if coverage else 0, components=False)
         y_parts.append(Yt[:, te[0]:te[-1] + 1] if np.all(np.diff(te) == 1) else Yt[:, te])

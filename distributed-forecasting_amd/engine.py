@@ -315,8 +315,38 @@ class Engine:
             self._vec_cache[key] = (sig_t, s_a, s_m, code)
         return self._vec_cache[key]
 
+    def series_priors(self, grid: DeviceGrid, n: int, changepoint_prior_scale=None,
+                      seasonality_prior_scale=None, holidays_prior_scale=None):
+        """Per-series prior scales for hyperparameter batching (the AutoML
+        ProphetHyperoptEstimator search space, notebooks/automl/...:111-123):
+        each argument is a scalar or an [n] array (None: this engine's
+        config).  Returns (tau [n], sigmas [n, K]) float64 device tensors for
+        ``fit(priors=...)``: Fourier columns get seasonality_prior_scale,
+        holiday columns holidays_prior_scale (UPSTREAM's per-holiday default)."""
+        dev = torch.device("cuda", self.device)
+        cfg = self.config
+
+        def vec(v, default):
+            a = np.broadcast_to(np.asarray(default if v is None else v, np.float64), (n,))
+            if not np.all(a > 0):
+                raise ValueError("prior scales must be positive")
+            return a
+        tau = vec(changepoint_prior_scale, cfg.changepoint_prior_scale)
+        sps = vec(seasonality_prior_scale, cfg.seasonality_prior_scale)
+        h = grid.holidays
+        nh = h.n if h is not None else 0
+        sig = np.empty((n, grid.K), np.float64)
+        sig[:, :grid.K - nh] = sps[:, None]
+        if nh:
+            if holidays_prior_scale is None:
+                sig[:, grid.K - nh:] = np.asarray(h.prior_scales, np.float64)[None, :]
+            else:
+                sig[:, grid.K - nh:] = vec(holidays_prior_scale, cfg.holidays_prior_scale)[:, None]
+        return (torch.from_numpy(np.ascontiguousarray(tau)).to(dev),
+                torch.from_numpy(sig).to(dev))
+
     def problem(self, grid: DeviceGrid, y_scaled: torch.Tensor, n: int,
-                cap_scaled: torch.Tensor | None = None) -> L.PfProblem:
+                cap_scaled: torch.Tensor | None = None, priors=None) -> L.PfProblem:
         sig, s_a, s_m, mode = self._vectors(grid)
         pb = L.PfProblem()
         pb.n_series = n
@@ -335,7 +365,14 @@ class Engine:
         for i in range(3):
             pb.fourier_orders[i] = fo[i]
         pb.season_mode = mode
-        pb._keep = (sig, s_a, s_m, y_scaled, cap_scaled)
+        pb.tau_series = pb.sigmas_series = None
+        if priors is not None:
+            tau_s, sig_s = priors
+            assert tau_s.dtype == torch.float64 and tuple(tau_s.shape) == (n,)
+            assert sig_s.dtype == torch.float64 and tuple(sig_s.shape) == (n, grid.K)
+            assert tau_s.is_contiguous() and sig_s.is_contiguous()
+            pb.tau_series, pb.sigmas_series = tau_s.data_ptr(), sig_s.data_ptr()
+        pb._keep = (sig, s_a, s_m, y_scaled, cap_scaled, priors)
         return pb
 
     def prepare(self, grid: DeviceGrid, Y: torch.Tensor, cap: torch.Tensor | None = None):
@@ -367,11 +404,11 @@ class Engine:
         return y_scale, y_scaled, theta, status, cap_scaled
 
     def objective_grad(self, grid: DeviceGrid, y_scaled: torch.Tensor, theta: torch.Tensor,
-                       cap_scaled: torch.Tensor | None = None):
+                       cap_scaled: torch.Tensor | None = None, priors=None):
         n = theta.shape[0]
         f = torch.empty(n, dtype=torch.float64, device=theta.device)
         g = torch.empty_like(theta)
-        pb = self.problem(grid, y_scaled, n, cap_scaled)
+        pb = self.problem(grid, y_scaled, n, cap_scaled, priors)
         rc = self.ctx.lib.pf_objective_grad(self.ctx.h, ctypes.byref(pb), _ptr(theta), _ptr(f),
                                             _ptr(g), _stream(self.device))
         self.ctx.check(rc, "pf_objective_grad")
@@ -391,14 +428,16 @@ class Engine:
         return o
 
     def fit(self, grid: DeviceGrid, Y: torch.Tensor, polish: bool = True,
-            stan_faithful: bool = False, cap: torch.Tensor | None = None, **opt) -> FitResult:
+            stan_faithful: bool = False, cap: torch.Tensor | None = None, priors=None,
+            **opt) -> FitResult:
         """Fit every row of Y [n, T_pad] (raw y, float64, on this GPU).
 
         Default: Stan L-BFGS warm-up (<= lbfgs_warmup iterations) handed to
         the exact-MAP polish (status PF_ST_MAP when certified; uncertified
         series resume L-BFGS).  ``stan_faithful=True`` first runs Stan's full
         termination rules (the reference's optimizer run), then polishes to
-        the same MAP; ``polish=False`` stops where Stan stops."""
+        the same MAP; ``polish=False`` stops where Stan stops.  ``priors``
+        (``series_priors``) gives every row its own prior scales."""
         n = Y.shape[0]
         y_scale, y_scaled, theta, status, cap_scaled = self.prepare(grid, Y, cap)
         dev = Y.device
@@ -406,7 +445,7 @@ class Engine:
         f_stan = torch.empty(n, dtype=torch.float64, device=dev)
         n_iter = torch.empty(n, dtype=torch.int32, device=dev)
         n_eval = torch.empty(n, dtype=torch.int32, device=dev)
-        pb = self.problem(grid, y_scaled, n, cap_scaled)
+        pb = self.problem(grid, y_scaled, n, cap_scaled, priors)
         o = self.fit_opts(polish, stan_faithful, **opt)
         rc = self.ctx.lib.pf_fit(self.ctx.h, ctypes.byref(pb), ctypes.byref(o), _ptr(theta),
                                  _ptr(f), _ptr(f_stan), _ptr(status), _ptr(n_iter), _ptr(n_eval),

@@ -83,6 +83,12 @@ typedef struct {
    *                1 = every column additive, 2 = mixed.                   */
   int32_t fourier_orders[3];
   int32_t season_mode;
+  /* Hyperparameter batching (the AutoML ProphetHyperoptEstimator search over
+   * changepoint / seasonality / holidays prior scales, notebooks/automl/
+   * 22-09-26-06:54-Prophet-...py:111-123, run as extra batch rows): per-series
+   * prior scales, or NULL to use the shared tau / sigmas above.            */
+  const double *tau_series;     /* [n_series]      changepoint_prior_scale   */
+  const double *sigmas_series;  /* [n_series * K]  per-column prior scales   */
 } pf_problem;
 
 typedef struct {

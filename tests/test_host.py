@@ -182,3 +182,26 @@ def test_synthetic_shape_and_determinism():
     assert np.array_equal(a, b) and a.min() >= 0 and np.all(a == np.round(a))
     df = synthetic.store_item_frame(2, 3)
     assert len(df) == 6 * 1826 and df["store"].dtype == np.int32
+
+
+# ------------------------------------------------ hyperparameter search layout
+def test_tuning_trials_and_layout():
+    from distributed_forecasting_amd import tuning
+    tr = tuning.sample_trials(64, seed=3)
+    assert len(tr) == 64
+    for t in tr:
+        for k in tuning.PRIOR_KEYS:
+            lo, hi = tuning.SEARCH_SPACE[k]
+            assert np.exp(lo) <= t[k] <= np.exp(hi)
+        assert t["seasonality_mode"] in ("additive", "multiplicative")
+    assert tr == tuning.sample_trials(64, seed=3)
+    lay = tuning.expand_trials(5, tr[:4], "multiplicative")
+    seen = []
+    for mode, (js, si, tj) in lay.items():
+        assert all(tr[j]["seasonality_mode"] == mode for j in js)
+        assert len(si) == len(tj) == 5 * len(js)
+        assert np.array_equal(si[:5], np.arange(5)) and set(tj) == set(js)
+        seen += js
+    assert sorted(seen) == [0, 1, 2, 3]
+    with pytest.raises(ValueError):
+        tuning.expand_trials(2, [dict(seasonality_mode="bogus")], "additive")
