@@ -327,7 +327,7 @@ class Engine:
         cfg = self.config
 
         def vec(v, default):
-            a = np.broadcast_to(np.asarray(default if v is None else v, np.float64), (n,))
+            a = np.array(np.broadcast_to(np.asarray(default if v is None else v, np.float64), (n,)))
             if not np.all(a > 0):
                 raise ValueError("prior scales must be positive")
             return a
