@@ -453,6 +453,28 @@ class Engine:
         self.ctx.check(rc, "pf_fit")
         return FitResult(grid, theta, y_scale, f, f_stan, status, n_iter, n_eval, self.config)
 
+    def forecast_async(self, stream: torch.cuda.Stream, fit: FitResult, ds_ns: np.ndarray,
+                       **predict_kw):
+        """Future grid + ``predict`` on ``stream``, ordered after the work
+        queued so far on the current stream (the fit), so the caller's next
+        fit overlaps this forecast: the forecast kernels fill the CUs that
+        the fit's tail leaves idle (the context's fit scratch is not touched
+        by the forecast).  The fit's tensors are recorded on ``stream`` so the
+        caching allocator does not hand them out before the forecast has read
+        them.  Outputs live on ``stream``: wait on it before using them."""
+        cur = torch.cuda.current_stream(fit.theta.device)
+        stream.wait_stream(cur)
+        g = fit.grid
+        for t in (fit.theta, fit.y_scale, fit.status, g.t, g.XT, g.t_change, g.seg, g.cp_first):
+            t.record_stream(stream)
+        for v in predict_kw.values():
+            if isinstance(v, torch.Tensor) and v.is_cuda:
+                v.record_stream(stream)
+        with torch.cuda.stream(stream):
+            fg = self.predict_grid(fit, ds_ns)
+            out = self.predict(fit, fg, **predict_kw)
+        return fg, out
+
     def predict_grid(self, fit: FitResult, ds_ns: np.ndarray) -> DeviceGrid:
         g = fit.grid
         return build_grid(ds_ns, g.seasons, start_ns=g.start_ns, t_scale_ns=g.t_scale_ns,

@@ -498,3 +498,23 @@ def test_partition_adapter_and_allocated_second_stage(eng):
     T = len(df.ds.unique())
     assert len(fine) == 4 * (T + 90 + 90)
     assert fine.groupby(["store", "item"]).size().eq(T + 180).all()
+
+
+def test_forecast_async_matches_same_stream(eng, golden_ref):
+    """Engine.forecast_async (forecast on a side stream, overlapping the next
+    fit) gives bit-identical outputs to the same-stream predict, also when
+    the next fit is queued before the forecast has run."""
+    ds, Y, fut = golden_ref["ds_ns"], golden_ref["Y"], golden_ref["fut_ns"]
+    g = _grid(eng, ds)
+    Yd = _Y(g, Y)
+    fit = eng.fit(g, Yd)
+    fg = eng.predict_grid(fit, fut)
+    ref = eng.predict(fit, fg, seed=3, components=False)
+    side = torch.cuda.Stream()
+    fg2, out = eng.forecast_async(side, fit, fut, seed=3, components=False)
+    del fit
+    fit2 = eng.fit(g, Yd)                  # overlaps the side-stream forecast
+    torch.cuda.current_stream().wait_stream(side)
+    for k in ("yhat", "yhat_lower", "yhat_upper"):
+        assert torch.equal(out[k][:, :fg2.T], ref[k][:, :fg.T]), k
+    assert torch.equal(fit2.theta, eng.fit(g, Yd).theta)
