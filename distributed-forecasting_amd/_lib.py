@@ -24,7 +24,7 @@ EXPORTED = ["pf_ctx_create", "pf_ctx_destroy", "pf_last_error", "pf_default_fit_
             "pf_fit", "pf_predict", "pf_set_timing", "pf_read_timings", "pf_cv_metrics"]
 PF_MAX_COMP = 32  # include/prophet_hip.h
 PF_INTERVAL = {"exact": 0, "sample": 1}
-CV_METRICS = ["mse", "rmse", "mae", "mape", "smape", "coverage"]
+CV_METRICS = ["mse", "rmse", "mae", "mape", "smape", "coverage", "mdape"]
 
 
 class EngineUnavailable(RuntimeError):

@@ -23,7 +23,7 @@ struct CvKArgs {
 };
 
 __global__ __launch_bounds__(64) void k_cv_metrics(CvKArgs a) {
-  __shared__ double s_sum[PF_CV_NMETRICS][PF_CV_GMAX];
+  __shared__ double s_sum[PF_CV_MDAPE][PF_CV_GMAX];
   __shared__ int s_cnt[PF_CV_GMAX];
   const int series = blockIdx.x, lane = pf_lane();
   const double *y = a.y + (size_t)series * a.n_rows;
@@ -55,7 +55,41 @@ __global__ __launch_bounds__(64) void k_cv_metrics(CvKArgs a) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) ymin = fmin(ymin, __shfl_xor(ymin, o, 64));
   __syncthreads();
-  if (lane < PF_CV_NMETRICS) {
+  // MDAPE (UPSTREAM rolling_median_by_h): lane g takes horizon groups g,
+  // g+64, ...; group i's sample is its rows extended backwards (rows are
+  // sorted by horizon) until the window is filled; a group is kept iff
+  // rows up to its end >= window (monotone: UPSTREAM's backward sweep stops
+  // at the first group that cannot fill it).  Median by rank counting.
+  {
+    double macc = 0.0, mcnt = 0.0;
+    for (int g = lane; g < a.n_groups; g += 64) {
+      const int gs = a.group_start[g], r1 = a.group_start[g + 1];
+      if (r1 < a.window) continue;
+      const int r0 = (r1 - gs >= a.window) ? gs : r1 - a.window;
+      const int n = r1 - r0, k0 = (n - 1) / 2, k1 = n / 2;
+      double v0 = NAN, v1 = NAN;
+      bool bad = false;
+      for (int j = r0; j < r1 && !bad; ++j) {
+        const double vj = fabs((y[j] - (double)yh[j]) / y[j]);
+        if (vj != vj) { bad = true; break; }
+        int lt = 0, le = 0;
+        for (int q = r0; q < r1; ++q) {
+          const double vq = fabs((y[q] - (double)yh[q]) / y[q]);
+          lt += (vq < vj);
+          le += (vq <= vj);
+        }
+        if (lt <= k0 && k0 < le) v0 = vj;
+        if (lt <= k1 && k1 < le) v1 = vj;
+      }
+      macc += bad ? NAN : (v0 + v1) * 0.5;
+      mcnt += 1.0;
+    }
+    macc = wave_sum(macc);
+    mcnt = wave_sum(mcnt);
+    if (lane == 0)
+      a.metrics[(size_t)series * PF_CV_NMETRICS + PF_CV_MDAPE] = (mcnt > 0.0) ? macc / mcnt : NAN;
+  }
+  if (lane < PF_CV_MDAPE) {
     const int m = lane;
     const double w = (double)a.window;
     double x_sum = 0.0, acc = 0.0;

@@ -224,9 +224,12 @@ int pf_predict(pf_ctx *ctx, const pf_predict_args *args, void *stream);
  * of the rolled values.  Rows (the concatenated fold predictions) must be
  * sorted by horizon; group_start[n_groups+1] delimits equal-horizon runs and
  * is shared by all series.  MAPE is NaN when min|y| < 1e-8 (UPSTREAM skips
- * it); coverage is NaN when yhat_lower/upper are NULL.                    */
+ * it); coverage is NaN when yhat_lower/upper are NULL.  MDAPE follows UPSTREAM
+ * rolling_median_by_h (AutoML logs it, notebooks/automl/...:163): per
+ * horizon group from the last, the median of the group's rows extended
+ * backwards to the window; groups that cannot fill the window are dropped. */
 enum { PF_CV_MSE = 0, PF_CV_RMSE = 1, PF_CV_MAE = 2, PF_CV_MAPE = 3, PF_CV_SMAPE = 4,
-       PF_CV_COVERAGE = 5, PF_CV_NMETRICS = 6 };
+       PF_CV_COVERAGE = 5, PF_CV_MDAPE = 6, PF_CV_NMETRICS = 7 };
 typedef struct {
   int32_t n_series, n_rows, n_groups, window;
   const int32_t *group_start;          /* [n_groups + 1], n_groups <= 512 */

@@ -628,6 +628,27 @@ def rolling_mean_by_h(x, h, w):
     return hs[trailing_i + 1:], res_x[trailing_i + 1:]
 
 
+def rolling_median_by_h(x, h, w):
+    """UPSTREAM diagnostics.rolling_median_by_h (prophet 1.0): from the last
+    horizon backwards, the median of the horizon's values extended with the
+    preceding rows (sorted order) until w values; stop at the first horizon
+    that cannot reach w."""
+    hs = np.unique(h)
+    res_h, res_x = [], []
+    for i in range(len(hs) - 1, -1, -1):
+        idx = np.flatnonzero(h == hs[i])
+        xs = list(x[idx])
+        nxt = idx[0] - 1
+        while len(xs) < w and nxt >= 0:
+            xs.append(x[nxt])
+            nxt -= 1
+        if len(xs) < w:
+            break
+        res_h.append(hs[i])
+        res_x.append(np.median(xs))
+    return np.array(res_h[::-1]), np.array(res_x[::-1])
+
+
 def performance_metrics(y, yhat, horizon, rolling_window=0.1,
                         metrics=("mse", "rmse", "mae", "mape"), yhat_lower=None,
                         yhat_upper=None):
@@ -662,6 +683,9 @@ def performance_metrics(y, yhat, horizon, rolling_window=0.1,
         sape = 2 * np.abs(yhat - y) / (np.abs(y) + np.abs(yhat))
         hs, v = rolling_mean_by_h(sape, horizon, w)
         out["smape"] = v
+    if "mdape" in metrics:
+        hs, v = rolling_median_by_h(np.abs((y - yhat) / y), horizon, w)
+        out["mdape"] = v
     if "coverage" in metrics and yhat_lower is not None:
         cov = ((y >= yhat_lower) & (y <= yhat_upper)).astype(np.float64)
         hs, v = rolling_mean_by_h(cov, horizon, w)

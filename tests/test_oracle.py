@@ -172,3 +172,12 @@ def test_order_statistic_spacings_match_sampling():
     assert stats.ks_2samp(bl, el).pvalue > 1e-3
     assert stats.ks_2samp(bh, eh).pvalue > 1e-3
     assert stats.ks_2samp(bh - bl, eh - el).pvalue > 1e-3
+
+
+def test_rolling_median_by_h_small():
+    """Known answers worked by hand from UPSTREAM rolling_median_by_h."""
+    x, h = np.array([1., 3., 5., 7., 9.]), np.array([1, 1, 2, 3, 3])
+    hs, v = po.rolling_median_by_h(x, h, 2)
+    assert hs.tolist() == [1, 2, 3] and v.tolist() == [2.0, 4.0, 8.0]
+    hs, v = po.rolling_median_by_h(x, h, 3)
+    assert hs.tolist() == [2, 3] and v.tolist() == [3.0, 7.0]
