@@ -54,7 +54,13 @@ class ParamsStore:
 
     def put_batch(self, fb: B.FittedBatch, keys: np.ndarray) -> str:
         """Persist the fits of one batch; ``keys`` [n, k] integer keys."""
-        rec = fb.to_record(np.asarray(keys, dtype=np.int64).reshape(fb.n, -1))
+        return self.put_record(fb.to_record(np.asarray(keys, dtype=np.int64).reshape(fb.n, -1)))
+
+    def put_record(self, rec: dict) -> str:
+        """Persist one record (``FittedBatch.to_record`` or
+        ``serialize.json_to_record`` fields, with ``keys``)."""
+        if "keys" not in rec:
+            raise ValueError("record needs integer 'keys' [n, k] to be indexed")
         name = f"bucket_{len(self.manifest['records']):06d}.npz"
         tmp = os.path.join(self.path, name + ".tmp.npz")
         np.savez(tmp, **rec)

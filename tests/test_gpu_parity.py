@@ -548,3 +548,34 @@ def test_cv_mdape_ragged_groups(eng, window):
         ape = np.abs((y[s] - f[s].astype(np.float64)) / y[s])
         _, v = po.rolling_median_by_h(ape, h, window)
         assert abs(m[s] - np.mean(v)) <= 1e-13 * abs(np.mean(v)), (s, m[s], np.mean(v))
+
+
+def test_prophet_json_export_import(eng, tmp_path):
+    """serialize.model_to_json (fbprophet 0.7.1 layout; parity unpinned: no
+    Prophet in the image) -> json_to_record -> ParamsStore -> PyFunc predict
+    reproduces the fitted model's yhat without refitting."""
+    import json
+    from distributed_forecasting_amd import serialize
+    df = synthetic.store_item_frame(1, 1)
+    m = dfa.reference_model()
+    m.fit(df[["ds", "y"]])
+    d = json.loads(serialize.model_to_json(m))
+    assert d["__fbprophet_version"] == "0.7.1"
+    for a in ("growth", "seasonality_mode", "y_scale", "interval_width", "component_modes"):
+        assert d[a] == getattr(m, a)
+    assert np.shape(d["params"]["delta"]) == (1, 25) and np.shape(d["params"]["beta"]) == (1, 26)
+    assert d["seasonalities"][0] == ["yearly", "weekly"]
+    fut = m.make_future_dataframe(periods=90, freq="d", include_history=True)
+    fc = m.predict(fut)
+    trend = np.asarray(d["params"]["trend"][0]) * m.y_scale
+    assert np.allclose(trend, fc["trend"].to_numpy()[:len(trend)], rtol=1e-6, atol=1e-6 * m.y_scale)  # forecast frame is f32
+    tcc = pd.read_json(__import__("io").StringIO(d["train_component_cols"]), orient="table")
+    assert tcc.shape == (26, 6) and tcc["multiplicative_terms"].sum() == 26
+    rec = serialize.json_to_record(json.dumps(d), keys=[7, 9])
+    assert np.array_equal(rec["theta"][0], m._batch.fit.theta[0].cpu().numpy())
+    store = dfa.ParamsStore(str(tmp_path / "imported"))
+    store.put_record(rec)
+    model = dfa.ForecastStoreItemModel(store, seed=0)
+    inp = pd.DataFrame({"ds": fut["ds"], "store": 7, "item": 9})
+    out = model.predict(None, inp)
+    assert np.allclose(out["yhat"].to_numpy(np.float64), fc["yhat"].to_numpy(), rtol=1e-5, atol=1e-3)

@@ -205,3 +205,36 @@ def test_tuning_trials_and_layout():
     assert sorted(seen) == [0, 1, 2, 3]
     with pytest.raises(ValueError):
         tuning.expand_trials(2, [dict(seasonality_mode="bogus")], "additive")
+
+
+def test_prophet_json_record_layout():
+    """serialize.json_to_record on a hand-built fbprophet-0.7.1-layout JSON
+    (host only): theta order [k, m, delta, log sigma_obs, beta], time units,
+    and the refusal of layouts the engine cannot serve."""
+    import json
+    from distributed_forecasting_amd import serialize
+    d = {"mcmc_samples": 0, "y_scale": 12.5, "start": 1356998400.0, "t_scale": 86400.0 * 1825,
+         "changepoints_t": [0.1, 0.5],
+         "history_dates": pd.Series(pd.date_range("2013-01-01", periods=3), name="ds")
+         .to_json(orient="split", date_format="iso"),
+         "seasonalities": [["weekly"], {"weekly": {"period": 7, "fourier_order": 1,
+                                                   "prior_scale": 10.0, "mode": "additive",
+                                                   "condition_name": None}}],
+         "extra_regressors": [[], {}],
+         "params": {"k": [[0.3]], "m": [[0.6]], "delta": [[0.01, -0.02]],
+                    "sigma_obs": [[0.05]], "beta": [[0.1, 0.2]]}}
+    rec = serialize.json_to_record(json.dumps(d), keys=[1, 2])
+    assert np.allclose(rec["theta"][0], [0.3, 0.6, 0.01, -0.02, np.log(0.05), 0.1, 0.2])
+    assert rec["start_ns"] == 1356998400 * 10**9 and rec["t_scale_ns"] == 1825 * NS_PER_DAY
+    assert rec["history_dates"][0] == pd.Timestamp("2013-01-01").value
+    assert list(rec["season_orders"]) == [1] and rec["keys"].shape == (1, 2)
+    t = np.linspace(0, 1, 5)
+    tr = serialize._trend(d["params"], t, np.array(d["changepoints_t"]), "linear")
+    want = [0.3 * x + 0.6 + sum(dl * (x - c) for dl, c in zip([0.01, -0.02], [0.1, 0.5]) if x >= c)
+            for x in t]
+    assert np.allclose(tr, want, rtol=0, atol=1e-15)
+    bad = dict(d, params=dict(d["params"], beta=[[0.1, 0.2, 0.3]]))
+    with pytest.raises(NotImplementedError, match="beyond the seasonal"):
+        serialize.json_to_record(json.dumps(bad))
+    with pytest.raises(NotImplementedError, match="mcmc"):
+        serialize.json_to_record(json.dumps(dict(d, mcmc_samples=10)))
