@@ -59,6 +59,8 @@ def _component_cols(model) -> pd.DataFrame:
     hol_cols = list(spec.names) if spec is not None else []
     cols = {name: [int(c == name) for c in comp_of] + [0] * len(hol_cols)
             for name in model.seasonalities}
+    for h in (spec.holidays if spec is not None else ()):
+        cols[h] = [0] * len(comp_of) + [int(c.split("_delim_")[0] == h) for c in hol_cols]
     if hol_cols:
         cols["holidays"] = [0] * len(comp_of) + [1] * len(hol_cols)
     row_comp = comp_of + ["holidays"] * len(hol_cols)
