@@ -21,7 +21,8 @@ PF_ST_CONSTANT = 50
 # Every symbol include/prophet_hip.h declares (checked by tests/test_abi.py).
 EXPORTED = ["pf_ctx_create", "pf_ctx_destroy", "pf_last_error", "pf_default_fit_opts",
             "pf_num_changepoints", "pf_build_grid", "pf_prepare", "pf_objective_grad",
-            "pf_fit", "pf_predict", "pf_set_timing", "pf_read_timings", "pf_cv_metrics"]
+            "pf_fit", "pf_predict", "pf_set_timing", "pf_read_timings", "pf_cv_metrics",
+            "pf_hessian"]
 PF_MAX_COMP = 32  # include/prophet_hip.h
 PF_INTERVAL = {"exact": 0, "sample": 1}
 CV_METRICS = ["mse", "rmse", "mae", "mape", "smape", "coverage", "mdape"]
@@ -112,6 +113,7 @@ def load(path: str = LIB_PATH):
     lib.pf_prepare.argtypes = [vp, ctypes.c_int, ctypes.POINTER(PfGrid), ctypes.c_int,
                                vp, vp, vp, vp, vp, vp, vp, vp]
     lib.pf_objective_grad.argtypes = [vp, ctypes.POINTER(PfProblem), vp, vp, vp, vp]
+    lib.pf_hessian.argtypes = [vp, ctypes.POINTER(PfProblem), vp, vp, vp]
     lib.pf_fit.argtypes = [vp, ctypes.POINTER(PfProblem), ctypes.POINTER(PfFitOpts),
                            vp, vp, vp, vp, vp, vp, vp]
     lib.pf_predict.argtypes = [vp, ctypes.POINTER(PfPredictArgs), vp]

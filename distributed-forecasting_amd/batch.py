@@ -150,6 +150,41 @@ class GridSpec:
     holidays: object = None     # HolidaySpec of the fit grid (None: no holiday columns)
 
 
+def holiday_record(spec) -> dict:
+    """HolidaySpec -> plain arrays for a params-store record (no pickles)."""
+    if spec is None or spec.n == 0:
+        return {}
+    return {"hol_names": np.array(spec.names), "hol_prior_scales": np.array(spec.prior_scales, np.float64),
+            "hol_holidays": np.array(spec.holidays),
+            "hol_rows": np.array(spec.rows, np.int64).reshape(-1, 2),
+            "hol_mode": np.str_(spec.mode)}
+
+
+def holiday_from_record(rec: dict):
+    """Inverse of ``holiday_record`` (None when the record has no holiday columns)."""
+    from .holidays import HolidaySpec
+    if "hol_names" not in rec:
+        return None
+    rows = tuple((int(j), int(d)) for j, d in np.asarray(rec["hol_rows"]).reshape(-1, 2))
+    return HolidaySpec(tuple(str(s) for s in rec["hol_names"]),
+                       tuple(float(v) for v in rec["hol_prior_scales"]),
+                       tuple(str(s) for s in rec["hol_holidays"]), rows, str(rec["hol_mode"]))
+
+
+def check_record_config(rec: dict, cfg) -> None:
+    """A record is served only under the settings it was fitted with (the
+    reference stores each run's full Prophet model: 02_training.py:193-196,
+    loaded whole at model_wrapper.py:58).  Raises ValueError on a mismatch of
+    growth, seasonality mode or interval width."""
+    for field, want in (("growth", cfg.growth), ("seasonality_mode", cfg.seasonality_mode)):
+        if field in rec and str(rec[field]) != str(want):
+            raise ValueError(f"record was fitted with {field}={str(rec[field])!r}; the store/engine "
+                             f"config has {field}={want!r}")
+    if "interval_width" in rec and abs(float(rec["interval_width"]) - float(cfg.interval_width)) > 1e-12:
+        raise ValueError(f"record interval_width={float(rec['interval_width'])} differs from the "
+                         f"config's {cfg.interval_width}")
+
+
 def _dense(A, n: int, T: int, T_pad: int, dev) -> torch.Tensor:
     """[n, T] numpy/tensor -> zero-padded [n, T_pad] float64 device tensor."""
     out = torch.zeros((n, T_pad), dtype=torch.float64, device=dev)
@@ -243,9 +278,17 @@ class FittedBatch:
 
     # -------------------------------------------------------- params store
     def to_record(self, keys: np.ndarray | None = None) -> dict:
-        """Host arrays describing the fits (one params-store bucket)."""
+        """Host arrays describing the fits (one params-store bucket): theta,
+        scales, the grid spec (seasonalities, changepoints, holiday columns)
+        and the model settings a forecast depends on (growth, seasonality
+        mode, interval width), so a record is never served with a
+        configuration it was not fitted under."""
         g = self.fit.grid
+        cfg = self.engine.config
         rec = {
+            "growth": np.str_(cfg.growth),
+            "seasonality_mode": np.str_(cfg.seasonality_mode),
+            "interval_width": np.float64(cfg.interval_width),
             "theta": self.fit.theta.cpu().numpy(),
             "y_scale": self.fit.y_scale.cpu().numpy(),
             "f": self.fit.f.cpu().numpy(),
@@ -259,23 +302,36 @@ class FittedBatch:
             "season_periods": np.array([s[1] for s in g.seasons], dtype=np.float64),
             "season_orders": np.array([s[2] for s in g.seasons], dtype=np.int64),
         }
+        rec.update(holiday_record(getattr(g, "holidays", None)))
         if keys is not None:
             rec["keys"] = np.asarray(keys, dtype=np.int64)
+            if self.series_ids is None:
+                rec["series_id"] = series_id(rec["keys"])
         if self.series_ids is not None:
             rec["series_id"] = self.series_ids.cpu().numpy()
         return rec
 
     @classmethod
     def from_record(cls, engine: E.Engine, rec: dict, rows=None) -> "FittedBatch":
-        """Rebuild a (sub-)batch from a params-store record without refitting."""
+        """Rebuild a (sub-)batch from a params-store record without refitting.
+        Raises ValueError if the record was fitted under a growth /
+        seasonality mode other than ``engine.config``'s or if theta's width
+        does not match the record's grid (3 + S + K)."""
+        check_record_config(rec, engine.config)
         dev = torch.device("cuda", engine.device)
         sel = slice(None) if rows is None else np.asarray(rows)
         theta = torch.from_numpy(np.ascontiguousarray(rec["theta"][sel])).to(dev)
         n = theta.shape[0]
         seasons = [(str(a), float(b), int(c)) for a, b, c in
                    zip(rec["season_names"], rec["season_periods"], rec["season_orders"])]
+        hol = holiday_from_record(rec)
+        K = sum(2 * o for _, _, o in seasons) + (hol.n if hol is not None else 0)
+        S = int(np.asarray(rec["t_change"]).shape[0])
+        if theta.shape[1] != 3 + S + K:
+            raise ValueError(f"record theta has {theta.shape[1]} columns; its grid needs "
+                             f"3 + S + K = {3 + S + K}")
         spec = GridSpec(seasons, int(rec["start_ns"]), int(rec["t_scale_ns"]),
-                        torch.from_numpy(np.ascontiguousarray(rec["t_change"])).to(dev))
+                        torch.from_numpy(np.ascontiguousarray(rec["t_change"])).to(dev), hol)
 
         def _t(name, dtype):
             return torch.from_numpy(np.ascontiguousarray(rec[name][sel]).astype(dtype)).to(dev)

@@ -39,7 +39,7 @@ struct pf_timed {
 struct pf_ctx {
   int device;
   char err[512];
-  void *ws;         // scratch owned by the context (polish per-row scalars)
+  void *ws;         // scratch owned by the context (lane-blocked grid copy)
   size_t ws_bytes;
   int timing;       // record events around launches
   int n_timed;      // records since the last pf_read_timings
@@ -349,7 +349,6 @@ struct FitKArgs {
   const double *tau_series, *sigmas_series;
   const double *y_scaled;
   const double *cap_scaled;  // [n][Tp] logistic capacity / y_scale (natural rows), else NULL
-  double *ws;  // polish workspace [n][3][Tp]
   // fit
   double *theta;
   double *f_out, *f_stan, *g_out;
@@ -470,6 +469,10 @@ template <int NW, int KMAX, int MODE = 2>
 struct FitSmem {
   static constexpr int NSET = ((MODE & 3) == 2) ? 2 : 1;  // (mult, add) gradient sets
   static constexpr int NL = NW * 64;                 // row-pass threads
+  // polish Hessian: beta column blocks of 16 and output tiles over
+  // [trend 2 blocks | beta NBB blocks] (pf_polish.h)
+  static constexpr int NBB = (KMAX + 15) / 16;
+  static constexpr int NTILE = (2 + NBB) * (3 + NBB) / 2;
   double *y;        // [ny] lane-blocked y_scaled (position r*NL + L)
   double *th;       // [128]
   double *kseg;     // [64]
@@ -483,29 +486,33 @@ struct FitSmem {
   double *fout;     // [4]
   double *sig;      // [4] sigma, 1/sigma^2 of the published point; [2] = this series' tau
   double *gpart;    // [NW][NSET*KMAX] per-wave beta-gradient totals
-  double *pd, *pz;  // [64] polish direction / scratch
+  double *pd, *pz;  // [128] polish direction / scratch (two parameter words)
   int *cpl;         // [64] per changepoint: owner thread
   int *qmap;        // [64]
   int *flag;        // [4] loop control
   double *ctc, *csg, *csm, *csa;  // [64] t_change[j], sigmas[f], s_m[f], s_a[f] (0 past the end)
   double *U;        // union region
   LbLds<ModeTr<MODE>::PW> *lb; // U view (Stan phase)
-  int LD;           // stride of H / M in U (polish)
+  int LD;           // stride of the polish matrix A in U
+  double *pmt, *prho;  // polish, logistic: [32][32] d m_s / d theta, [32] segment sums
   static __host__ __device__ size_t fixed_doubles(int ny) {
     return (size_t)ny + 64 * 4 + 2 * KMAX + 2 * NL + 2 * NW + 128 + NW + 128 + 4 + 4 +
-           (size_t)NW * NSET * KMAX + 128 + 32 + 32 + 4 + 4 * 64;
+           (size_t)NW * NSET * KMAX + 256 + 32 + 32 + 4 + 4 * 64;
+  }
+  // polish region: A (P rows + 8 padding rows, stride LD) overlapping the
+  // tile-reduction buffer, then the logistic tables
+  static __host__ __device__ size_t polish_head_doubles(int P) {
+    const size_t a = (size_t)(P + 8) * (size_t)(P | 1);
+    const size_t red = (size_t)NTILE * 4 * 64;
+    return ((a > red ? a : red) + 1) & ~(size_t)1;
   }
   static __host__ __device__ size_t union_bytes(int P, int S, bool polish) {
     (void)S;
     const size_t lbb = sizeof(LbLds<ModeTr<MODE>::PW>) + 16;
     if (!polish) return lbb;
-    const size_t tiles = (size_t)10 * 4 * 64 * sizeof(double);
-    const int LD = P | 1;
-    // H, A + 8 padding rows (80.7 KB with the fixed part at P = 54, T = 1826:
-    // two workgroups per CU)
-    const size_t hm = (2 * (size_t)P + 8) * LD * sizeof(double);
-    size_t u = lbb > tiles ? lbb : tiles;
-    return u > hm ? u : hm;
+    const size_t extra = ((MODE & PF_MODE_LOGI) != 0) ? (32 * 32 + 32) : 0;
+    const size_t hm = (polish_head_doubles(P) + extra) * sizeof(double);
+    return lbb > hm ? lbb : hm;
   }
   static __host__ __device__ size_t bytes(int ny, int P, int S, bool polish) {
     return fixed_doubles(ny) * sizeof(double) + union_bytes(P, S, polish) + 64;
@@ -529,8 +536,8 @@ struct FitSmem {
     fout = p; p += 4;
     sig = p; p += 4;
     gpart = p; p += (size_t)NW * NSET * KMAX;
-    pd = p; p += 64;
-    pz = p; p += 64;
+    pd = p; p += 128;
+    pz = p; p += 128;
     cpl = reinterpret_cast<int *>(p); p += 32;
     qmap = reinterpret_cast<int *>(p); p += 32;
     flag = reinterpret_cast<int *>(p); p += 4;
@@ -544,6 +551,8 @@ struct FitSmem {
     U = reinterpret_cast<double *>(base + off);
     lb = reinterpret_cast<LbLds<ModeTr<MODE>::PW> *>(U);
     LD = P | 1;
+    pmt = U + polish_head_doubles(P);
+    prho = pmt + 32 * 32;
   }
 };
 
@@ -1555,25 +1564,60 @@ __device__ __forceinline__ void polish_body(const FitKArgs &a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   FitSmem<NW, KMAX, MODE> sm;
   sm.carve(smem_raw, a.TQ, a.P);
+  constexpr int PW = ModeTr<MODE>::PW;
   const int s = blockIdx.x, lane = pf_lane();
   const int P = a.P;
   const int st = a.status[s];
   if (st == PF_ST_CONSTANT || st == PF_ST_BADINIT || st == PF_ST_MAP) return;
   double *th_out = a.theta + (size_t)s * P;
   load_y<NW, KMAX, MODE>(a, sm, s);
-  double x = (lane < P) ? th_out[lane] : 0.0;
+  PV<PW> x, g;
+#pragma unroll
+  for (int h = 0; h < PW; ++h) x[h] = (lane + 64 * h < P) ? th_out[lane + 64 * h] : 0.0;
   __syncthreads();
-  double f, g;
-  const bool bad = eval_collective1<NW, KMAX, O0, O1, O2, MODE>(a, sm, x, f, g);
+  double f;
+  const bool bad = eval_collective<NW, KMAX, O0, O1, O2, MODE>(a, sm, x, f, g);
   if (bad) return;
   int n_eval = 1, n_newton = 0;  // polish evaluations are not counted in n_eval[]
   const bool cert = polish_run<NW, KMAX, O0, O1, O2, MODE>(a, sm, x, f, g, n_eval, n_newton);
   if (threadIdx.x < 64) {
-    if (lane < P) th_out[lane] = x;
+#pragma unroll
+    for (int h = 0; h < PW; ++h)
+      if (lane + 64 * h < P) th_out[lane + 64 * h] = x[h];
     if (lane == 0) {
       a.f_out[s] = f;
       if (cert) a.status[s] = PF_ST_MAP;
     }
+  }
+}
+
+// Exact Hessian of the smooth part at theta (pf_hessian; the polish's model
+// without damping): H_out[s][P][P].
+template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
+__global__ __launch_bounds__(NW * 64) void k_hessian(FitKArgs a, double *H_out) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  FitSmem<NW, KMAX, MODE> sm;
+  sm.carve(smem_raw, a.TQ, a.P);
+  constexpr int PW = ModeTr<MODE>::PW;
+  const int s = blockIdx.x, lane = pf_lane();
+  const int P = a.P, S = a.S;
+  load_y<NW, KMAX, MODE>(a, sm, s);
+  PV<PW> x, g;
+#pragma unroll
+  for (int h = 0; h < PW; ++h) x[h] = (lane + 64 * h < P) ? a.theta[(size_t)s * P + lane + 64 * h] : 0.0;
+  __syncthreads();
+  double f;
+  (void)eval_collective<NW, KMAX, O0, O1, O2, MODE>(a, sm, x, f, g);
+  PV<PW> gh = g;
+  const double c = 1.0 / sm.sig[2];
+  if (lane >= 2 && lane < 2 + S) gh[0] = g[0] - c * (double)((x[0] > 0.0) - (x[0] < 0.0));
+  hessian_collective<NW, KMAX, O0, O1, O2, MODE>(a, sm, x, gh, 0.0);
+  __syncthreads();
+  const int LD = sm.LD;
+  double *Ho = H_out + (size_t)s * P * P;
+  for (int e = threadIdx.x; e < P * P; e += NW * 64) {
+    const int i = e / P, j = e - i * P;
+    Ho[e] = sm.U[i * LD + j];
   }
 }
 
@@ -1595,11 +1639,11 @@ __global__ __launch_bounds__(NW * 64, FitOcc<KMAX>::W) void k_fit_resume(FitKArg
   fit_body<NW, KMAX, O0, O1, O2, MODE>(a, a.pass, a.o, a.warm_cap != 0);
 }
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
-__global__ __launch_bounds__(NW * 64, 2) void k_polish(FitKArgs a) {
+__global__ __launch_bounds__(NW * 64, FitOcc<KMAX>::W) void k_polish(FitKArgs a) {
   polish_body<NW, KMAX, O0, O1, O2, MODE>(a);
 }
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
-__global__ __launch_bounds__(NW * 64, 2) void k_polish_resume(FitKArgs a) {
+__global__ __launch_bounds__(NW * 64, FitOcc<KMAX>::W) void k_polish_resume(FitKArgs a) {
   polish_body<NW, KMAX, O0, O1, O2, MODE>(a);
 }
 // The warm-up hand-off of launch_fitlike — L-BFGS warm-up -> polish, once
@@ -1622,7 +1666,7 @@ __device__ __noinline__ void polish_phase(const FitKArgs &a) {
   polish_body<NW, KMAX, O0, O1, O2, MODE>(a);
 }
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
-__global__ __launch_bounds__(NW * 64, 2) void k_fit_polish(FitKArgs a) {
+__global__ __launch_bounds__(NW * 64, FitOcc<KMAX>::W) void k_fit_polish(FitKArgs a) {
   const int W = a.o.lbfgs_warmup;
   for (int ps = 0; ps < 3; ++ps) {
     const bool warm = ps < 2;
@@ -1892,7 +1936,7 @@ void pf_default_fit_opts(pf_fit_opts *o) {
   o->max_iter = 10000;
   o->history = 5;
   o->polish = 1;
-  o->polish_max_iter = 20;
+  o->polish_max_iter = 50;  // accepted Newton steps (damped logistic fits from far away need ~30)
   o->lbfgs_warmup = 60;
   o->lbfgs_warmup_evals = 0;
 }
@@ -2016,21 +2060,33 @@ FitKArgs make_fit_args(const pf_problem *pb) {
   return a;
 }
 
+enum { PF_LAUNCH_OBJGRAD = 0, PF_LAUNCH_FIT = 1, PF_LAUNCH_HESSIAN = 2 };
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
-int launch_fitlike(pf_ctx *ctx, bool fit, const FitKArgs &a, int n, hipStream_t st) {
-  // the polish handles K <= 32 and 2 + S <= 32 (J space of two 32-column blocks)
-  constexpr bool HAS_POLISH = KMAX <= 32 && (MODE & PF_MODE_LOGI) == 0;
+int launch_fitlike(pf_ctx *ctx, int what, const FitKArgs &a, int n, hipStream_t st, double *H_out) {
+  // the polish handles K <= 48 (three 16-column beta blocks) and 2 + S <= 32
+  constexpr bool HAS_POLISH = KMAX <= 48;
   const size_t smem = FitSmem<NW, KMAX, MODE>::bytes(a.TQ, a.P, a.S, false);
   const size_t smem_p = FitSmem<NW, KMAX, MODE>::bytes(a.TQ, a.P, a.S, HAS_POLISH);
   if (smem > 160 * 1024) return set_err(ctx, "fit: series too long for the LDS budget");
-  if (fit) {
+  if (what == PF_LAUNCH_HESSIAN) {
+    if constexpr (HAS_POLISH) {
+      if (2 + a.S > 32 || smem_p > 160 * 1024) return set_err(ctx, "pf_hessian: needs 2 + S <= 32 and the polish LDS budget");
+      auto kh = k_hessian<NW, KMAX, O0, O1, O2, MODE>;
+      PF_HIP(ctx, hipFuncSetAttribute((const void *)kh, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem_p));
+      PF_TIMED_LAUNCH(ctx, "k_hessian", n, st, kh, dim3(n), dim3(NW * 64), smem_p, st, a, H_out);
+      PF_HIP(ctx, hipGetLastError());
+      return 0;
+    } else {
+      return set_err(ctx, "pf_hessian: layout has no polish (K > 48)");
+    }
+  }
+  if (what == PF_LAUNCH_FIT) {
     void (*kf[2])(FitKArgs) = {k_fit<NW, KMAX, O0, O1, O2, MODE>,
                                k_fit_resume<NW, KMAX, O0, O1, O2, MODE>};
     for (int v = 0; v < 2; ++v)
       PF_HIP(ctx, hipFuncSetAttribute((const void *)kf[v],
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
-    bool polish = a.o.polish && a.ws && a.growth == PF_GROWTH_LINEAR && a.K <= 32 && 2 + a.S <= 32 &&
-                  smem_p <= 160 * 1024;
+    bool polish = a.o.polish && a.K <= 48 && 2 + a.S <= 32 && smem_p <= 160 * 1024;
     void (*kpl[2])(FitKArgs) = {nullptr, nullptr};
     if constexpr (HAS_POLISH) {
       kpl[0] = k_polish<NW, KMAX, O0, O1, O2, MODE>;
@@ -2097,8 +2153,8 @@ int launch_fitlike(pf_ctx *ctx, bool fit, const FitKArgs &a, int n, hipStream_t 
 //   (26, 10,3,0, ADD/MIXED) — same grid, other seasonality modes
 //   (34, 10,3,4, MULT) — sub-daily data (yearly + weekly + daily 4; config 5)
 //   dense fallbacks KMAX 32 / 61 (any K <= KMAX), features read from X^T.
-int dispatch_fitlike(pf_ctx *ctx, bool fit, const FitKArgs &a, int n, const int32_t *orders, int mode,
-                     hipStream_t st) {
+int dispatch_fitlike(pf_ctx *ctx, int fit, const FitKArgs &a, int n, const int32_t *orders, int mode,
+                     hipStream_t st, double *H_out = nullptr) {
   const bool o1030 = orders[0] == 10 && orders[1] == 3 && orders[2] == 0;
   const bool o1034 = orders[0] == 10 && orders[1] == 3 && orders[2] == 4;
   constexpr int LG = PF_MODE_LOGI, WD = PF_MODE_WIDE;
@@ -2107,32 +2163,32 @@ int dispatch_fitlike(pf_ctx *ctx, bool fit, const FitKArgs &a, int n, const int3
   // (P <= 72: two parameter words per lane) — SURVEY.md §8d configs[4]
   if (o1030 && a.K > 26 && a.K <= 36 && mode == MODE_MULT) {
     if (a.growth == PF_GROWTH_LOGISTIC)
-      return launch_fitlike<PF_FIT_NW, 36, 10, 3, 0, MODE_MULT | LG>(ctx, fit, a, n, st);
-    return launch_fitlike<PF_FIT_NW, 36, 10, 3, 0, MODE_MULT>(ctx, fit, a, n, st);
+      return launch_fitlike<PF_FIT_NW, 36, 10, 3, 0, MODE_MULT | LG>(ctx, fit, a, n, st, H_out);
+    return launch_fitlike<PF_FIT_NW, 36, 10, 3, 0, MODE_MULT>(ctx, fit, a, n, st, H_out);
   }
   if (o1034 && a.K > 34 && a.K <= 44 && mode == MODE_MULT) {
     if (a.growth == PF_GROWTH_LOGISTIC)
-      return launch_fitlike<PF_FIT_NW, 44, 10, 3, 4, MODE_MULT | LG | WD>(ctx, fit, a, n, st);
-    return launch_fitlike<PF_FIT_NW, 44, 10, 3, 4, MODE_MULT | WD>(ctx, fit, a, n, st);
+      return launch_fitlike<PF_FIT_NW, 44, 10, 3, 4, MODE_MULT | LG | WD>(ctx, fit, a, n, st, H_out);
+    return launch_fitlike<PF_FIT_NW, 44, 10, 3, 4, MODE_MULT | WD>(ctx, fit, a, n, st, H_out);
   }
   if (a.P > 64) return set_err(ctx, "fit: P > 64 is supported for yearly+weekly+daily (10,3,4) plus <= 10 extra columns, multiplicative");
   if (a.growth == PF_GROWTH_LOGISTIC) {
     if (o1030 && a.K == 26 && mode == MODE_MULT)
-      return launch_fitlike<PF_FIT_NW, 26, 10, 3, 0, MODE_MULT | LG>(ctx, fit, a, n, st);
+      return launch_fitlike<PF_FIT_NW, 26, 10, 3, 0, MODE_MULT | LG>(ctx, fit, a, n, st, H_out);
     if (o1034 && a.K == 34 && mode == MODE_MULT)
-      return launch_fitlike<PF_FIT_NW, 34, 10, 3, 4, MODE_MULT | LG>(ctx, fit, a, n, st);
-    if (a.K <= 32) return launch_fitlike<PF_FIT_NW, 32, 0, 0, 0, MODE_MIXED | LG>(ctx, fit, a, n, st);
+      return launch_fitlike<PF_FIT_NW, 34, 10, 3, 4, MODE_MULT | LG>(ctx, fit, a, n, st, H_out);
+    if (a.K <= 32) return launch_fitlike<PF_FIT_NW, 32, 0, 0, 0, MODE_MIXED | LG>(ctx, fit, a, n, st, H_out);
     return set_err(ctx, "fit: logistic growth supports K <= 32, or yearly+weekly+daily (K = 34) multiplicative");
   }
   if (o1030 && a.K == 26) {
-    if (mode == MODE_MULT) return launch_fitlike<PF_FIT_NW, 26, 10, 3, 0, MODE_MULT>(ctx, fit, a, n, st);
-    if (mode == MODE_ADD) return launch_fitlike<PF_FIT_NW, 26, 10, 3, 0, MODE_ADD>(ctx, fit, a, n, st);
-    return launch_fitlike<PF_FIT_NW, 26, 10, 3, 0, MODE_MIXED>(ctx, fit, a, n, st);
+    if (mode == MODE_MULT) return launch_fitlike<PF_FIT_NW, 26, 10, 3, 0, MODE_MULT>(ctx, fit, a, n, st, H_out);
+    if (mode == MODE_ADD) return launch_fitlike<PF_FIT_NW, 26, 10, 3, 0, MODE_ADD>(ctx, fit, a, n, st, H_out);
+    return launch_fitlike<PF_FIT_NW, 26, 10, 3, 0, MODE_MIXED>(ctx, fit, a, n, st, H_out);
   }
   if (o1034 && a.K == 34 && mode == MODE_MULT)
-    return launch_fitlike<PF_FIT_NW, 34, 10, 3, 4, MODE_MULT>(ctx, fit, a, n, st);
-  if (a.K <= 32) return launch_fitlike<PF_FIT_NW, 32, 0, 0, 0, MODE_MIXED>(ctx, fit, a, n, st);
-  if (a.K <= 61) return launch_fitlike<PF_FIT_NW, 61, 0, 0, 0, MODE_MIXED>(ctx, fit, a, n, st);
+    return launch_fitlike<PF_FIT_NW, 34, 10, 3, 4, MODE_MULT>(ctx, fit, a, n, st, H_out);
+  if (a.K <= 32) return launch_fitlike<PF_FIT_NW, 32, 0, 0, 0, MODE_MIXED>(ctx, fit, a, n, st, H_out);
+  if (a.K <= 61) return launch_fitlike<PF_FIT_NW, 61, 0, 0, 0, MODE_MIXED>(ctx, fit, a, n, st, H_out);
   return set_err(ctx, "fit: K > 61 not supported");
 }
 
@@ -2142,19 +2198,17 @@ extern "C" {
 
 // Context scratch for one fit-like call: [lane-blocked grid | polish rows],
 // then the permutation launch (stream-ordered with the fit that reads it).
-static int prepare_fit_scratch(pf_ctx *ctx, FitKArgs &a, int n_series, bool polish, hipStream_t st) {
+static int prepare_fit_scratch(pf_ctx *ctx, FitKArgs &a, hipStream_t st) {
   const size_t TQ = (size_t)a.TQ;
   size_t gbytes = TQ * sizeof(double) * (1 + (size_t)a.K) + TQ * sizeof(int32_t);
   gbytes = (gbytes + 255) & ~(size_t)255;
-  const size_t pbytes = polish ? (size_t)n_series * 3 * a.Tp * sizeof(double) : 0;
   void *w = nullptr;
-  const int rc = ctx_workspace(ctx, gbytes + pbytes, &w);
+  const int rc = ctx_workspace(ctx, gbytes, &w);
   if (rc) return rc;
   double *base = (double *)w;
   a.tP = base;
   a.XTP = base + TQ;
   a.sgP = (int32_t *)(base + TQ * (1 + (size_t)a.K));
-  a.ws = polish ? (double *)((char *)w + gbytes) : nullptr;
   const int nb = (int)((TQ + 255) / 256);
   PF_TIMED_LAUNCH(ctx, "k_permute_grid", nb, st, k_permute_grid, dim3(nb), dim3(256), 0, st,
                   a.t, a.seg, a.XT, a.T, a.Tp, a.K, a.S, a.R, PF_FIT_NW * 64,
@@ -2191,9 +2245,9 @@ int pf_objective_grad(pf_ctx *ctx, const pf_problem *pb, const double *theta, do
   a.theta = const_cast<double *>(theta);
   a.f_out = f;
   a.g_out = g;
-  rc = prepare_fit_scratch(ctx, a, pb->n_series, false, (hipStream_t)stream);
+  rc = prepare_fit_scratch(ctx, a, (hipStream_t)stream);
   if (rc) return rc;
-  return dispatch_fitlike(ctx, false, a, pb->n_series, pb->fourier_orders, mode_of(pb),
+  return dispatch_fitlike(ctx, PF_LAUNCH_OBJGRAD, a, pb->n_series, pb->fourier_orders, mode_of(pb),
                           (hipStream_t)stream);
 }
 
@@ -2213,10 +2267,23 @@ int pf_fit(pf_ctx *ctx, const pf_problem *pb, const pf_fit_opts *opts, double *t
   a.n_iter = n_iter;
   a.n_eval = n_eval;
   a.o = *opts;
-  rc = prepare_fit_scratch(ctx, a, pb->n_series, opts->polish != 0, (hipStream_t)stream);
+  rc = prepare_fit_scratch(ctx, a, (hipStream_t)stream);
   if (rc) return rc;
-  return dispatch_fitlike(ctx, true, a, pb->n_series, pb->fourier_orders, mode_of(pb),
+  return dispatch_fitlike(ctx, PF_LAUNCH_FIT, a, pb->n_series, pb->fourier_orders, mode_of(pb),
                           (hipStream_t)stream);
+}
+
+int pf_hessian(pf_ctx *ctx, const pf_problem *pb, const double *theta, double *H, void *stream) {
+  int rc = check_problem(ctx, pb);
+  if (rc) return rc;
+  if (!theta || !H) return set_err(ctx, "pf_hessian: NULL buffer");
+  if (pb->n_series == 0) return 0;
+  FitKArgs a = make_fit_args(pb);
+  a.theta = const_cast<double *>(theta);
+  rc = prepare_fit_scratch(ctx, a, (hipStream_t)stream);
+  if (rc) return rc;
+  return dispatch_fitlike(ctx, PF_LAUNCH_HESSIAN, a, pb->n_series, pb->fourier_orders, mode_of(pb),
+                          (hipStream_t)stream, H);
 }
 
 int pf_predict(pf_ctx *ctx, const pf_predict_args *p, void *stream) {

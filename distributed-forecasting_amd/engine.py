@@ -414,6 +414,18 @@ class Engine:
         self.ctx.check(rc, "pf_objective_grad")
         return f, g
 
+    def hessian(self, grid: DeviceGrid, y_scaled: torch.Tensor, theta: torch.Tensor,
+                cap_scaled: torch.Tensor | None = None, priors=None) -> torch.Tensor:
+        """[n, P, P] exact Hessian of the smooth part of the -log posterior at
+        theta (pf_hessian: the polish's model; Stan's Newton fallback)."""
+        n, P = theta.shape
+        H = torch.empty((n, P, P), dtype=torch.float64, device=theta.device)
+        pb = self.problem(grid, y_scaled, n, cap_scaled, priors)
+        rc = self.ctx.lib.pf_hessian(self.ctx.h, ctypes.byref(pb), _ptr(theta), _ptr(H),
+                                     _stream(self.device))
+        self.ctx.check(rc, "pf_hessian")
+        return H
+
     def fit_opts(self, polish: bool = True, stan_faithful: bool = False, **over) -> L.PfFitOpts:
         """pf_fit_opts: Stan optimizing() defaults + the engine's polish.
         ``stan_faithful`` runs Stan's full L-BFGS termination rules before the
@@ -421,7 +433,11 @@ class Engine:
         o = L.PfFitOpts()
         self.ctx.lib.pf_default_fit_opts(ctypes.byref(o))
         o.polish = 1 if polish else 0
-        if stan_faithful:
+        if stan_faithful or self.config.growth == "logistic":
+            # logistic growth: the warm-up hand-off can certify a worse local
+            # optimum than Stan's full run reaches (measured: tests/golden/
+            # golden_configs4.npz f_warm60_polish, 1 of 8 series 2.6e-4
+            # worse), so the polish starts where Stan's full L-BFGS stops
             o.lbfgs_warmup = 0
         for k, v in over.items():
             setattr(o, k, v)
@@ -492,6 +508,11 @@ class Engine:
         stream so the intervals do not depend on the batch composition."""
         n = fit.theta.shape[0]
         dev = fit.theta.device
+        if fit.theta.shape[1] != 3 + fgrid.S + fgrid.K:
+            # the kernel reads theta with stride 3 + S + K of the forecast grid
+            raise ValueError(f"theta has {fit.theta.shape[1]} columns but the forecast grid has "
+                             f"3 + S + K = {3 + fgrid.S + fgrid.K} (holiday / extra columns "
+                             f"missing from the grid?)")
         ns = self.config.uncertainty_samples if n_samples is None else n_samples
         sig, s_a, s_m, _ = self._vectors(fgrid)
         out = {k: torch.empty((n, fgrid.T_pad), dtype=torch.float32, device=dev)

@@ -178,7 +178,9 @@ class Prophet:
         S = int(tc.shape[0])
         K = th.shape[0] - 3 - S
         placed = getattr(g, "n_changepoints_placed", S)
-        self.changepoints_t = tc if placed > 0 else np.array([])
+        # UPSTREAM set_changepoints: with no changepoints placed the model
+        # keeps the dummy changepoints_t = [0] (delta then has one column)
+        self.changepoints_t = tc if placed > 0 else np.array([0.0])
         cp_idx = getattr(g, "cp_idx", None)
         if placed > 0 and cp_idx is not None and fb.fit_ds is not None:
             cp_ds = fb.fit_ds[cp_idx.cpu().numpy()[:placed]]

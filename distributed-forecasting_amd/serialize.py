@@ -110,18 +110,35 @@ def json_to_record(text: str, keys=None) -> dict:
     """Prophet-format JSON -> params-store record of one series (the fields
     ``FittedBatch.to_record`` writes; theta = [k, m, delta, log sigma_obs, beta]).
 
-    Only layouts the engine can serve are accepted: growth linear/flat/logistic,
-    seasonalities with their own Fourier columns (no conditions), no extra
+    The record carries the model's growth, seasonality mode and interval
+    width; ``ParamsStore.put_record`` refuses it when they differ from the
+    store's configuration (an additive fit is never served as multiplicative).
+    Only layouts the engine can serve are accepted: growth linear/flat/logistic
+    (logistic: the serving input must carry ``cap``), one mode shared by every
+    seasonality, seasonalities with their own Fourier columns (no conditions),
+    holidays (columns rebuilt from the model's holidays frame), no extra
     regressors, MAP fits (``mcmc_samples == 0``)."""
+    from .batch import holiday_record, series_id
+    from .holidays import holiday_spec
     d = json.loads(text)
     if int(d.get("mcmc_samples") or 0) > 0:
         raise NotImplementedError("mcmc_samples > 0 fits cannot be served (MAP only)")
+    growth = str(d.get("growth", "linear"))
+    if growth not in ("linear", "flat", "logistic"):
+        raise NotImplementedError(f"growth {growth!r} cannot be served")
+    if d.get("logistic_floor"):
+        raise NotImplementedError("logistic floor is not supported")
     names, seas = d["seasonalities"]
     if d.get("extra_regressors") and d["extra_regressors"][0]:
         raise NotImplementedError("extra regressors are not supported")
     for n in names:
         if seas[n].get("condition_name"):
             raise NotImplementedError("conditional seasonalities are not supported")
+    mode = str(d.get("seasonality_mode", "additive"))
+    modes = {str(seas[n].get("mode", mode)) for n in names}
+    if len(modes) > 1 or (modes and modes.pop() != mode):
+        raise NotImplementedError("seasonalities with their own mode (not seasonality_mode) "
+                                  "cannot be served")
     p = d["params"]
     theta = np.concatenate([np.asarray(p["k"], np.float64).reshape(-1)[:1],
                             np.asarray(p["m"], np.float64).reshape(-1)[:1],
@@ -130,11 +147,22 @@ def json_to_record(text: str, keys=None) -> dict:
                             np.asarray(p["beta"], np.float64).reshape(-1)])
     P_seas = sum(2 * int(seas[n]["fourier_order"]) for n in names)
     S = len(d["changepoints_t"])
-    if theta.shape[0] - 3 - S != P_seas:
-        raise NotImplementedError("beta has columns beyond the seasonal Fourier features "
-                                  "(holidays/regressors): not importable")
+    spec = None
+    if d.get("holidays"):
+        hdf = pd.read_json(StringIO(d["holidays"]), orient="table")
+        cm = d.get("component_modes") or {}
+        hmode = "multiplicative" if "holidays" in cm.get("multiplicative", []) else (
+            "additive" if "holidays" in cm.get("additive", []) else mode)
+        spec = holiday_spec(hdf, float(d.get("holidays_prior_scale", 10.0)), hmode)
+    n_hol = spec.n if spec is not None else 0
+    if theta.shape[0] - 3 - S != P_seas + n_hol:
+        raise NotImplementedError("beta has columns beyond the seasonal Fourier features and "
+                                  "holidays (extra regressors?): not importable")
     hd = pd.read_json(StringIO(d["history_dates"]), typ="series", orient="split")
     rec = {
+        "growth": np.str_(growth),
+        "seasonality_mode": np.str_(mode),
+        "interval_width": np.float64(d.get("interval_width", 0.8)),
         "theta": theta[None, :],
         "y_scale": np.array([float(d["y_scale"])]),
         "f": np.array([np.nan]),
@@ -148,6 +176,9 @@ def json_to_record(text: str, keys=None) -> dict:
         "season_periods": np.array([float(seas[n]["period"]) for n in names]),
         "season_orders": np.array([int(seas[n]["fourier_order"]) for n in names], np.int64),
     }
+    rec.update(holiday_record(spec))
     if keys is not None:
         rec["keys"] = np.asarray(keys, np.int64).reshape(1, -1)
+        # same per-series Monte-Carlo stream as a fit made here (batch.series_id)
+        rec["series_id"] = series_id(rec["keys"])
     return rec

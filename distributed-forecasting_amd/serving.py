@@ -10,11 +10,23 @@ Here the fits of a whole bucket are one ``.npz`` record in a directory (no
 pickles: plain arrays, read with ``allow_pickle=False``), and the serving
 model batches every (store, item) group of its input that shares a record
 and a date set into one forecast launch.
+
+Several writers may share one store directory (torchrun ranks calling
+``forecast_store_items(params_store=..., rank, world_size)``, Spark executors
+running ``forecast_partitions(params_store=...)`` on a shared path): every
+record gets a name unique to its writer (``rec_<time ns>_<writer>_<seq>.npz``,
+written to a private temporary name and moved into place atomically), and the
+index is a scan of the directory — there is no shared mutable manifest.
+``manifest.json`` holds only the store's model configuration, written once
+when the store is created (identical content from every creator).  Later
+records win for a key that was refitted (names sort by creation time).
 """
 from __future__ import annotations
 
 import json
 import os
+import time
+import uuid
 
 import numpy as np
 import pandas as pd
@@ -24,33 +36,37 @@ from . import engine as E
 from .forecaster import get_engine
 
 MANIFEST = "manifest.json"
+REC_PREFIX = "rec_"
 
 
 class ParamsStore:
     """Directory of per-bucket fit records, indexed by integer series keys."""
 
-    def __init__(self, path: str, config: E.ProphetConfig | None = None):
+    def __init__(self, path: str, config: E.ProphetConfig | None = None, writer: str | None = None):
         self.path = path
         os.makedirs(path, exist_ok=True)
         mf = os.path.join(path, MANIFEST)
         if os.path.exists(mf):
             with open(mf) as f:
                 self.manifest = json.load(f)
+            if config is not None and E.ProphetConfig(**self.manifest["config"]) != config:
+                raise ValueError(f"params store {path!r} holds fits made with a different "
+                                 f"ProphetConfig: {self.manifest['config']}")
         else:
-            self.manifest = {"records": [], "config": (config or E.ProphetConfig.reference()).__dict__}
-            self._write_manifest()
+            self.manifest = {"config": (config or E.ProphetConfig.reference()).__dict__, "format": 2}
+            tmp = os.path.join(path, f".{MANIFEST}.{uuid.uuid4().hex}")
+            with open(tmp, "w") as f:
+                json.dump(self.manifest, f, indent=1, default=str)
+            os.replace(tmp, mf)
+        self.writer = writer or f"p{os.getpid()}{uuid.uuid4().hex[:8]}"
+        self._seq = 0
         self._records = {}
         self._index = None
+        self._index_names = None
 
     @property
     def config(self) -> E.ProphetConfig:
         return E.ProphetConfig(**self.manifest["config"])
-
-    def _write_manifest(self):
-        tmp = os.path.join(self.path, MANIFEST + ".tmp")
-        with open(tmp, "w") as f:
-            json.dump(self.manifest, f, indent=1, default=str)
-        os.replace(tmp, os.path.join(self.path, MANIFEST))
 
     def put_batch(self, fb: B.FittedBatch, keys: np.ndarray) -> str:
         """Persist the fits of one batch; ``keys`` [n, k] integer keys."""
@@ -58,17 +74,24 @@ class ParamsStore:
 
     def put_record(self, rec: dict) -> str:
         """Persist one record (``FittedBatch.to_record`` or
-        ``serialize.json_to_record`` fields, with ``keys``)."""
+        ``serialize.json_to_record`` fields, with ``keys``).  Raises
+        ValueError if the record was fitted under a growth, seasonality mode
+        or interval width other than this store's configuration."""
         if "keys" not in rec:
             raise ValueError("record needs integer 'keys' [n, k] to be indexed")
-        name = f"bucket_{len(self.manifest['records']):06d}.npz"
-        tmp = os.path.join(self.path, name + ".tmp.npz")
+        B.check_record_config(rec, self.config)
+        name = f"{REC_PREFIX}{time.time_ns():020d}_{self.writer}_{self._seq:06d}.npz"
+        self._seq += 1
+        tmp = os.path.join(self.path, f".{name}.{uuid.uuid4().hex}.tmp.npz")
         np.savez(tmp, **rec)
         os.replace(tmp, os.path.join(self.path, name))
-        self.manifest["records"].append(name)
-        self._write_manifest()
         self._index = None
         return name
+
+    def record_names(self) -> list:
+        """Every committed record of every writer, oldest first."""
+        return sorted(f for f in os.listdir(self.path)
+                      if f.startswith(REC_PREFIX) and f.endswith(".npz"))
 
     def record(self, name: str) -> dict:
         if name not in self._records:
@@ -78,13 +101,15 @@ class ParamsStore:
 
     def index(self) -> dict:
         """key tuple -> (record name, row); later records win (refits)."""
-        if self._index is None:
+        names = self.record_names()
+        if self._index is None or names != self._index_names:
             idx = {}
-            for name in self.manifest["records"]:
+            for name in names:
                 keys = self.record(name)["keys"]
                 for r, k in enumerate(map(tuple, keys.tolist())):
                     idx[k] = (name, r)
             self._index = idx
+            self._index_names = names
         return self._index
 
     def __len__(self):
@@ -117,16 +142,21 @@ class ForecastStoreItemModel:
     def predict(self, context, model_input: pd.DataFrame) -> pd.DataFrame:
         """model_wrapper.py:43-73, batched over every (store, item) group in
         ``model_input``.  Returns [ds, store, item, yhat, yhat_upper,
-        yhat_lower]; each group's rows sorted by ds (Prophet.predict order)."""
+        yhat_lower]; each group's rows sorted by ds (Prophet.predict order).
+        Logistic-growth stores need a ``cap`` column (UPSTREAM predict)."""
         for c in ("ds", "store", "item"):
             if c not in model_input:
                 raise ValueError(f"model_input must have column {c!r}")
         store = self._store
         eng = get_engine(store.config, self._device)
+        logistic = store.config.growth == "logistic"
+        if logistic and "cap" not in model_input:
+            raise ValueError('Capacities must be supplied for logistic growth in column "cap"')
         idx = store.index()
         kv = np.stack([model_input["store"].to_numpy(np.int64),
                        model_input["item"].to_numpy(np.int64)], axis=1)
         ds_all = B.to_ns(model_input["ds"])
+        cap_all = model_input["cap"].to_numpy(np.float64) if logistic else None
         order = np.lexsort((ds_all, kv[:, 1], kv[:, 0]))
         sk = kv[order]
         brk = np.flatnonzero(np.any(sk[1:] != sk[:-1], axis=1)) + 1
@@ -142,13 +172,16 @@ class ForecastStoreItemModel:
             name, row = idx[key]
             ds = ds_all[order[s:e]]
             jk = (name, ds.tobytes())
-            jobs.setdefault(jk, (ds, [], []))
+            jobs.setdefault(jk, (ds, [], [], []))
             jobs[jk][1].append(row)
             jobs[jk][2].append(key)
+            if logistic:
+                jobs[jk][3].append(cap_all[order[s:e]])
         frames = []
-        for (name, _), (ds, rows, keys) in jobs.items():
+        for (name, _), (ds, rows, keys, caps) in jobs.items():
             fb = B.FittedBatch.from_record(eng, store.record(name), rows)
-            Tf, out = fb.predict(ds, seed=self._seed, components=False)
+            Tf, out = fb.predict(ds, seed=self._seed, components=False,
+                                 cap=np.stack(caps) if logistic else None)
             n = len(rows)
             keys = np.asarray(keys, dtype=np.int64)
             fr = {"ds": np.tile(ds.astype("datetime64[ns]"), n),

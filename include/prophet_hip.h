@@ -165,6 +165,15 @@ int pf_prepare(pf_ctx *ctx, int n_series, const pf_grid *grid, int growth,
 int pf_objective_grad(pf_ctx *ctx, const pf_problem *pb, const double *theta,
                       double *f, double *g, void *stream);
 
+/* ------------------------------------------- exact Hessian (polish model)
+ * H[n*P*P] (row-major per series) = Hessian of the smooth part of the
+ * -log posterior at theta (the L1 term on delta excluded): the model the
+ * exact-MAP polish of pf_fit solves its QP with, and what Stan's Newton
+ * optimizer (PyStan optimizing(algorithm='Newton'), Prophet's fallback when
+ * L-BFGS fails, UPSTREAM) would form.  Linear, flat and logistic growth;
+ * needs 2 + S <= 32 and K <= 48.                                          */
+int pf_hessian(pf_ctx *ctx, const pf_problem *pb, const double *theta, double *H, void *stream);
+
 /* -------------------------------------------------- K3: batched fit (MAP)
  * theta_inout[n*P]: init in, optimum out.  f_out[n] final -log posterior,
  * f_stan[n] objective where the (first) L-BFGS phase stopped, status[n]

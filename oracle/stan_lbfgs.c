@@ -19,7 +19,8 @@
  *     tol_rel_obj 1e4, tol_grad 1e-8, tol_rel_grad 1e7, tol_param 1e-8,
  *     iter 1e4 (Prophet passes iter=1e4).
  * PARITY UNPINNED at the iteration level (no Stan here); the optimum is
- * certified against scipy L-BFGS-B in tests/test_oracle_fit.py.
+ * certified against scipy L-BFGS-B in tests/test_oracle.py
+ * (test_map_certified).
  *
  * Parameter vector (Stan unconstrained order):
  *   theta = [k, m, delta[S], log(sigma_obs), beta[K]],  P = 3 + S + K.
@@ -530,58 +531,143 @@ int orc_owlqn_fit2(const orc_problem *pb, int max_iter, double tol_rel_f, double
  * Each iteration: exact Hessian of the smooth part h, the lasso-QP subproblem
  *   min_z gh.(z-x) + 1/2 (z-x)' H (z-x) + c ||z_delta||_1
  * solved exactly by an active-set method (Cholesky solves on the free set),
- * then Armijo backtracking on the true objective.  Linear growth only.
+ * then Armijo backtracking on the true objective.  Linear, flat and logistic growth.
  * The HIP kernel (pf_polish.h) implements the same algorithm.
  * ------------------------------------------------------------------------- */
 #define PMAX 128
 
-/* Hessian of h (smooth part of -log posterior) at theta, linear growth. */
+/* Hessian of h (smooth part of -log posterior) at theta: linear, flat and
+ * logistic growth.  With r = y - mu and sigma^2 = exp(2 l):
+ *   H = (1/sigma^2) sum_i [dmu_i dmu_i' - r_i d2mu_i] + prior Hessian,
+ * plus the l row/column.  Trend parameters (k, m, delta) enter mu through
+ *   linear:   tr = k_s t + m_s              dmu/dth_t = u D_t
+ *   logistic: tr = cap sigmoid(z), z = k_s (t - m_s) with m_s from
+ *             UPSTREAM logistic_gamma;      dmu/dth_t = u cap s' dz
+ * where dz = (t - m_s) E_s - k_s M_s, E_s = dk_s/dth_t, M_s = dm_s/dth_t
+ * (recursion through logistic_gamma), and the second derivative adds
+ *   - r u cap [s'' dz dz' + s' d2z],  d2z = -(E_s M_s' + M_s E_s') - k_s D2M_s.
+ * The per-row terms are the rank-one updates below; the d2z terms collapse
+ * to per-segment sums rho_s = sum_{i in s} r_i u_i cap_i s'_i.  Same
+ * formulas as the HIP kernel's Hessian (pf_polish.h), checked against
+ * central differences of orc_objective's gradient in tests/test_oracle.py. */
+#define HMAXS 64
 int orc_hessian(const orc_problem *pb, const double *theta, double *H /*P*P*/, double *rr_out) {
-    const int T = pb->T, K = pb->K, S = pb->S, P = 3 + S + K, na = 2 + S, il = 2 + S;
-    if (pb->growth != 0 || P > PMAX) return -1;
+    const int T = pb->T, K = pb->K, S = pb->S, P = 3 + S + K, nt = 2 + S, il = 2 + S;
+    const int g = pb->growth;
+    if (P > PMAX || S + 1 > HMAXS) return -1;
     const double k = theta[0], m = theta[1];
     const double *delta = theta + 2, *beta = theta + 3 + S;
     const double sig2 = exp(2.0 * theta[il]);
-    double J[PMAX], D[PMAX];
+    static __thread double ks[HMAXS], ms[HMAXS], Mt[HMAXS][HMAXS], rho[HMAXS];
+    double dz[PMAX], Jb[PMAX], Wb[PMAX], Jr[PMAX];
     for (int a = 0; a < P * P; ++a) H[a] = 0.0;
-    double rr = 0.0;
-    double Jr[PMAX];
     for (int p = 0; p < P; ++p) Jr[p] = 0.0;
+    /* segment rates / offsets and (logistic) dm_s/dth_t */
+    ks[0] = k;
+    for (int j = 0; j < S; ++j) ks[j + 1] = ks[j] + delta[j];
+    ms[0] = m;
+    for (int s = 0; s <= S; ++s) { rho[s] = 0.0; for (int c = 0; c < nt; ++c) Mt[s][c] = 0.0; }
+    Mt[0][1] = 1.0;
+    if (g == 1) {
+        for (int s = 0; s < S; ++s) {
+            const double q = ks[s] / ks[s + 1], b = ks[s + 1];
+            ms[s + 1] = ms[s] + (pb->t_change[s] - ms[s]) * (1 - q);
+            for (int c = 0; c < nt; ++c) {
+                const double Es = (c == 0 || (c >= 2 && c - 2 < s)) ? 1.0 : 0.0;
+                const double Es1 = (c == 0 || (c >= 2 && c - 2 < s + 1)) ? 1.0 : 0.0;
+                const double dq = Es / b - ks[s] * Es1 / (b * b);
+                Mt[s + 1][c] = q * Mt[s][c] + (ms[s] - pb->t_change[s]) * dq;
+            }
+        }
+    }
+    double rr = 0.0;
     for (int i = 0; i < T; ++i) {
         const double *x = pb->X + (size_t)i * K;
         const double ti = pb->t[i];
         double xbm = 0.0, xba = 0.0;
         for (int f = 0; f < K; ++f) { xbm += x[f] * beta[f] * pb->s_m[f]; xba += x[f] * beta[f] * pb->s_a[f]; }
-        double ad = 0.0, atd = 0.0;
-        D[0] = ti; D[1] = 1.0;
-        for (int j = 0; j < S; ++j) {
-            if (ti >= pb->t_change[j]) { ad += delta[j]; atd -= pb->t_change[j] * delta[j]; D[2 + j] = ti - pb->t_change[j]; }
-            else D[2 + j] = 0.0;
-        }
-        const double tr = (k + ad) * ti + (m + atd);
+        int s = 0;
+        for (int j = 0; j < S; ++j) if (ti >= pb->t_change[j]) s = j + 1;
         const double u = 1.0 + xbm;
+        double tr, wt, gf = 1.0, sp = 0.0, sg = 0.0, capi = 0.0;
+        for (int c = 0; c < nt; ++c) dz[c] = 0.0;
+        if (g == 0) {
+            double ad = 0.0, atd = 0.0;
+            for (int j = 0; j < S; ++j)
+                if (ti >= pb->t_change[j]) { ad += delta[j]; atd -= pb->t_change[j] * delta[j]; dz[2 + j] = ti - pb->t_change[j]; }
+            tr = (k + ad) * ti + (m + atd);
+            dz[0] = ti;
+            dz[1] = 1.0;
+        } else if (g == 1) {
+            capi = pb->cap[i];
+            const double z = ks[s] * (ti - ms[s]);
+            sg = 1.0 / (1.0 + exp(-z));
+            sp = sg * (1.0 - sg);
+            tr = capi * sg;
+            for (int c = 0; c < nt; ++c) {
+                const double Es = (c == 0 || (c >= 2 && c - 2 < s)) ? 1.0 : 0.0;
+                dz[c] = (ti - ms[s]) * Es - ks[s] * Mt[s][c];
+            }
+            gf = capi * sp;
+        } else {
+            tr = m;
+            dz[1] = 1.0;
+        }
         const double r = pb->y[i] - (tr * u + xba);
         rr += r * r;
-        /* J without the l column: [a (na) | beta (K)] */
-        int q = 0;
-        for (int a = 0; a < na; ++a) J[q++] = D[a] * u;
-        for (int f = 0; f < K; ++f) J[q++] = x[f] * (tr * pb->s_m[f] + pb->s_a[f]);
-        const int nj = q;
-        for (int a = 0; a < nj; ++a) Jr[a] += J[a] * r;
-        /* accumulate J'J into the (l-excluded) index space mapped to theta */
-        for (int a = 0; a < nj; ++a) {
-            const int pa = a < na ? a : a + 1;
-            for (int b = 0; b <= a; ++b) {
-                const int pb_ = b < na ? b : b + 1;
-                H[pa * P + pb_] += J[a] * J[b];
+        if (g == 1) {
+            const double spp = sp * (1.0 - 2.0 * sg);
+            const double a = u * capi * sp;
+            wt = a * a - r * u * capi * spp;
+            rho[s] += r * u * capi * sp;
+        } else {
+            wt = u * u;
+        }
+        for (int f = 0; f < K; ++f) {
+            const double kf = tr * pb->s_m[f] + pb->s_a[f];
+            Jb[f] = x[f] * kf;
+            Wb[f] = x[f] * (u * kf - r * pb->s_m[f]);
+        }
+        for (int c = 0; c < nt; ++c) Jr[c] += r * u * gf * dz[c];
+        for (int f = 0; f < K; ++f) Jr[nt + 1 + f] += r * Jb[f];
+        for (int a = 0; a < nt; ++a) {
+            for (int b = 0; b <= a; ++b) H[a * P + b] += wt * dz[a] * dz[b];
+            for (int f = 0; f < K; ++f) H[(nt + 1 + f) * P + a] += gf * dz[a] * Wb[f];
+        }
+        for (int f = 0; f < K; ++f)
+            for (int f2 = 0; f2 <= f; ++f2) H[(nt + 1 + f) * P + nt + 1 + f2] += Jb[f] * Jb[f2];
+    }
+    if (g == 1) {
+        /* sum_s rho_s [E_s M_s' + M_s E_s' + k_s D2M_s], D2M by recursion */
+        static __thread double D2[HMAXS][HMAXS];
+        for (int a = 0; a < nt; ++a) for (int b = 0; b < nt; ++b) D2[a][b] = 0.0;
+        for (int s = 0; s <= S; ++s) {
+            if (s > 0) {
+                const int sp_ = s - 1;
+                const double q = ks[sp_] / ks[s], b = ks[s];
+                for (int a = 0; a < nt; ++a)
+                    for (int c = 0; c < nt; ++c) {
+                        const double Ea = (a == 0 || (a >= 2 && a - 2 < sp_)) ? 1.0 : 0.0;
+                        const double Ea1 = (a == 0 || (a >= 2 && a - 2 < s)) ? 1.0 : 0.0;
+                        const double Ec = (c == 0 || (c >= 2 && c - 2 < sp_)) ? 1.0 : 0.0;
+                        const double Ec1 = (c == 0 || (c >= 2 && c - 2 < s)) ? 1.0 : 0.0;
+                        const double dqa = Ea / b - ks[sp_] * Ea1 / (b * b);
+                        const double dqc = Ec / b - ks[sp_] * Ec1 / (b * b);
+                        const double d2q = -(Ea * Ec1 + Ea1 * Ec) / (b * b) + 2.0 * ks[sp_] * Ea1 * Ec1 / (b * b * b);
+                        D2[a][c] = q * D2[a][c] + dqa * Mt[sp_][c] + Mt[sp_][a] * dqc +
+                                   (ms[sp_] - pb->t_change[sp_]) * d2q;
+                    }
+            }
+            for (int a = 0; a < nt; ++a) {
+                const double Ea = (a == 0 || (a >= 2 && a - 2 < s)) ? 1.0 : 0.0;
+                for (int b = 0; b <= a; ++b) {
+                    const double Eb = (b == 0 || (b >= 2 && b - 2 < s)) ? 1.0 : 0.0;
+                    H[a * P + b] += rho[s] * (Ea * Mt[s][b] + Mt[s][a] * Eb + ks[s] * D2[a][b]);
+                }
             }
         }
-        /* residual cross term  -r * d2mu/(da dbeta) = -r D_a X_f s_m */
-        for (int a = 0; a < na; ++a)
-            for (int f = 0; f < K; ++f)
-                H[(na + 1 + f) * P + a] -= r * D[a] * x[f] * pb->s_m[f];
     }
-    /* symmetrize, scale by 1/sigma^2 */
+    /* symmetrize, scale by 1/sigma^2 (l row excluded: set below) */
     for (int a = 0; a < P; ++a)
         for (int b = 0; b < a; ++b) { H[a * P + b] /= sig2; H[b * P + a] = H[a * P + b]; }
     for (int a = 0; a < P; ++a) H[a * P + a] /= sig2;
@@ -589,15 +675,36 @@ int orc_hessian(const orc_problem *pb, const double *theta, double *H /*P*P*/, d
     H[0] += 1.0 / 25.0;
     H[1 * P + 1] += 1.0 / 25.0;
     for (int f = 0; f < K; ++f) H[(3 + S + f) * P + 3 + S + f] += 1.0 / (pb->sigmas[f] * pb->sigmas[f]);
-    /* l row/col: d2h/dl2 = 8 sigma^2 + 2 Q / sigma^2 ; d2h/dl dp = 2/sigma^2 sum r dmu/dp */
+    /* l row/col: d2h/dl2 = 8 sigma^2 + 2 Q / sigma^2 ; d2h/dl dp = (2/sigma^2) sum r dmu/dp */
     H[il * P + il] = 8.0 * sig2 + 2.0 * rr / sig2;
-    for (int a = 0; a < P - 1; ++a) {
-        const int pa = a < na ? a : a + 1;
-        const double v = 2.0 * Jr[a] / sig2;
-        H[il * P + pa] = v;
-        H[pa * P + il] = v;
+    for (int p = 0; p < P; ++p) {
+        if (p == il) continue;
+        const double v = 2.0 * Jr[p] / sig2;
+        H[il * P + p] = v;
+        H[p * P + il] = v;
     }
     if (rr_out) *rr_out = rr;
+    return 0;
+}
+
+/* Central-difference Hessian of the smooth gradient (check for orc_hessian;
+ * relative step h per coordinate, L1 term's gradient removed by its sign at
+ * the perturbed point). */
+int orc_hessian_fd(const orc_problem *pb, const double *theta, double h, double *H) {
+    const int S = pb->S, P = 3 + S + pb->K;
+    if (P > PMAX) return -1;
+    double xp[PMAX], gp[PMAX], gm[PMAX], f;
+    for (int q = 0; q < P; ++q) {
+        const double e = h * fmax(1.0, fabs(theta[q]));
+        memcpy(xp, theta, P * sizeof(double));
+        xp[q] = theta[q] + e;
+        if (orc_objective(pb, xp, &f, gp)) return -2;
+        for (int j = 0; j < S; ++j) gp[2 + j] -= sgn(xp[2 + j]) / pb->tau;
+        xp[q] = theta[q] - e;
+        if (orc_objective(pb, xp, &f, gm)) return -2;
+        for (int j = 0; j < S; ++j) gm[2 + j] -= sgn(xp[2 + j]) / pb->tau;
+        for (int p = 0; p < P; ++p) H[p * P + q] = (gp[p] - gm[p]) / (2.0 * e);
+    }
     return 0;
 }
 
@@ -692,28 +799,46 @@ int orc_qp_active(const double *H, const double *gh, const double *x, int P, int
     return nsolve;
 }
 
-int orc_polish(const orc_problem *pb, double *theta, int max_it, double *f_out,
-               int *n_newton, int *n_eval, int *n_solve) {
+/* Proximal Newton with Levenberg-Marquardt damping: when the QP under the
+ * exact Hessian hits a non-positive pivot (the objective is not convex away
+ * from the optimum: multiplicative seasonality, logistic trend), the model is
+ * H + lam * dmax * I with lam raised x10 until the active-set QP solves; lam
+ * is relaxed /10 after every accepted step.  Any positive-definite model
+ * predicts zero decrease exactly at a KKT point, so the certificate
+ * (dec >= -1e-15 |f| after a QP solved to KKT) is unchanged.  cert_out = 1
+ * when the loop ended on that certificate. */
+int orc_polish_ex(const orc_problem *pb, double *theta, int max_it, int damp, double *f_out,
+                  int *n_newton, int *n_eval, int *n_solve, int *cert_out) {
     const int S = pb->S, P = 3 + S + pb->K;
     const double c = 1.0 / pb->tau;
-    if (pb->growth != 0 || P > PMAX) return -1;
-    static __thread double H[PMAX * PMAX];
+    if (P > PMAX) return -1;
+    static __thread double H[PMAX * PMAX], Hd[PMAX * PMAX];
     double g[PMAX], gh[PMAX], z[PMAX], d[PMAX], xn[PMAX], gn[PMAX], f, fn = 0.0;
     evaluator ev = {pb, 0};
     if (feval(&ev, theta, &f, g)) return -2;
-    int it, ns = 0;
+    int it, ns = 0, cert = 0, nn = 0;
+    double lam = 0.0;
     for (it = 0; it < max_it; ++it) {
         for (int p = 0; p < P; ++p) gh[p] = g[p];
         for (int j = 0; j < S; ++j) gh[2 + j] -= c * sgn(theta[2 + j]);
         if (orc_hessian(pb, theta, H, NULL)) break;
-        const int r = orc_qp_active(H, gh, theta, P, 2, S, c, z, 200);
+        double dmax = 0.0;
+        for (int p = 0; p < P; ++p) dmax = fmax(dmax, fabs(H[p * P + p]));
+        int r = -1;
+        for (int tr = 0; tr < 16; ++tr) {
+            memcpy(Hd, H, (size_t)P * P * sizeof(double));
+            for (int p = 0; p < P; ++p) Hd[p * P + p] += lam * dmax;
+            r = orc_qp_active(Hd, gh, theta, P, 2, S, c, z, 200);
+            if (r >= 0 || !damp) break;
+            lam = (lam == 0.0) ? 1e-10 : lam * 10.0;
+        }
         if (r < 0) break;
         ns += r;
         double l1z = 0.0, l1x = 0.0, dec = 0.0;
         for (int p = 0; p < P; ++p) { d[p] = z[p] - theta[p]; dec += gh[p] * d[p]; }
         for (int j = 0; j < S; ++j) { l1z += fabs(z[2 + j]); l1x += fabs(theta[2 + j]); }
         dec += c * (l1z - l1x);
-        if (dec > -1e-15 * fabs(f)) break;
+        if (dec > -1e-15 * fabs(f)) { cert = 1; break; }
         double alpha = 1.0;
         int ok = 0;
         for (int ls = 0; ls < 30; ++ls) {
@@ -722,13 +847,21 @@ int orc_polish(const orc_problem *pb, double *theta, int max_it, double *f_out,
             alpha *= 0.5;
         }
         if (!ok) break;
+        ++nn;
         memcpy(theta, xn, P * sizeof(double));
         memcpy(g, gn, P * sizeof(double));
         f = fn;
+        lam = (lam < 1e-9) ? 0.0 : lam * 0.1;
     }
     *f_out = f;
-    *n_newton = it;
+    *n_newton = nn;
     *n_eval = ev.n_eval;
     *n_solve = ns;
+    if (cert_out) *cert_out = cert;
     return 0;
+}
+
+int orc_polish(const orc_problem *pb, double *theta, int max_it, double *f_out,
+               int *n_newton, int *n_eval, int *n_solve) {
+    return orc_polish_ex(pb, theta, max_it, 0, f_out, n_newton, n_eval, n_solve, NULL);
 }

@@ -148,7 +148,8 @@ def certify(pb: po.Problem, theta_start, ftol=1e-15, gtol=1e-10, maxiter=20000):
 
 
 def hessian(pb: po.Problem, theta):
-    """Exact Hessian of the smooth part of f (linear growth) — orc_hessian."""
+    """Exact Hessian of the smooth part of f (linear, flat, logistic growth) —
+    orc_hessian (analytic, incl. the second derivatives through logistic_gamma)."""
     pin = _Pinned(pb)
     th = np.ascontiguousarray(theta, np.float64)
     P = th.shape[0]
@@ -156,28 +157,47 @@ def hessian(pb: po.Problem, theta):
     rc = lib().orc_hessian(ctypes.byref(pin.c), th.ctypes.data_as(ctypes.c_void_p),
                            H.ctypes.data_as(ctypes.c_void_p), None)
     if rc:
-        raise ValueError("orc_hessian: linear growth only")
+        raise ValueError(f"orc_hessian failed ({rc})")
     return H
 
 
-def polish(pb: po.Problem, theta, max_it=20):
+def hessian_fd(pb: po.Problem, theta, h=1e-6):
+    """Central differences of the smooth gradient (the check for ``hessian``)."""
+    pin = _Pinned(pb)
+    th = np.ascontiguousarray(theta, np.float64)
+    P = th.shape[0]
+    H = np.zeros((P, P))
+    rc = lib().orc_hessian_fd(ctypes.byref(pin.c), th.ctypes.data_as(ctypes.c_void_p),
+                              ctypes.c_double(h), H.ctypes.data_as(ctypes.c_void_p))
+    if rc:
+        raise ValueError(f"orc_hessian_fd failed ({rc})")
+    return H
+
+
+def polish(pb: po.Problem, theta, max_it=20, damp=False, return_cert=False):
     """Exact-MAP proximal-Newton polish (engine extension; same algorithm as
-    the HIP kernel).  Returns (theta, f, n_newton, n_eval, n_solve)."""
+    the HIP kernel).  ``damp``: Levenberg-Marquardt damping when the exact
+    Hessian model is not positive definite.  Returns (theta, f, n_newton,
+    n_eval, n_solve[, certified])."""
     pin = _Pinned(pb)
     th = np.array(theta, dtype=np.float64, copy=True)
     f = ctypes.c_double()
-    nn, ne, ns = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-    rc = lib().orc_polish(ctypes.byref(pin.c), th.ctypes.data_as(ctypes.c_void_p), int(max_it),
-                          ctypes.byref(f), ctypes.byref(nn), ctypes.byref(ne), ctypes.byref(ns))
+    nn, ne, ns, cert = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    rc = lib().orc_polish_ex(ctypes.byref(pin.c), th.ctypes.data_as(ctypes.c_void_p), int(max_it),
+                             int(bool(damp)), ctypes.byref(f), ctypes.byref(nn), ctypes.byref(ne),
+                             ctypes.byref(ns), ctypes.byref(cert))
     if rc:
         raise ValueError(f"orc_polish failed ({rc})")
-    return th, f.value, nn.value, ne.value, ns.value
+    out = (th, f.value, nn.value, ne.value, ns.value)
+    return out + (bool(cert.value),) if return_cert else out
 
 
-def fit_map(setup: po.FitSetup, opts=None, polish_it=20):
-    """Engine semantics on the CPU: Stan L-BFGS, then the exact-MAP polish."""
+def fit_map(setup: po.FitSetup, opts=None, polish_it=50, damp=True):
+    """Engine semantics on the CPU: Stan L-BFGS, then the exact-MAP polish
+    (every growth mode; Levenberg-Marquardt damping where the Hessian model
+    is not positive definite, as the kernel does)."""
     th, f, st, it, ne = fit_setup(setup, opts)
-    if setup.constant or setup.problem.growth != 0:
+    if setup.constant:
         return th, f, st, it, ne, f
-    th2, f2, nn, ne2, ns = polish(setup.problem, th, polish_it)
+    th2, f2, nn, ne2, ns = polish(setup.problem, th, polish_it, damp=damp)
     return th2, f2, st, it, ne + ne2, f

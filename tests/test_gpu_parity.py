@@ -579,3 +579,55 @@ def test_prophet_json_export_import(eng, tmp_path):
     inp = pd.DataFrame({"ds": fut["ds"], "store": 7, "item": 9})
     out = model.predict(None, inp)
     assert np.allclose(out["yhat"].to_numpy(np.float64), fc["yhat"].to_numpy(), rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("case", ["no_changepoints", "two_rows"])
+def test_prophet_json_roundtrip_dummy_changepoint(case, tmp_path):
+    """with no changepoints placed (n_changepoints=0, or a
+    2-row history) the model keeps UPSTREAM's dummy changepoints_t = [0]
+    beside a one-column delta; model_to_json works and json_to_record reads
+    our own export back (served yhat equals predict)."""
+    import json
+    from distributed_forecasting_amd import serialize
+    if case == "no_changepoints":
+        df = synthetic.store_item_frame(1, 1, "2016-01-01", "2017-12-31")[["ds", "y"]]
+        m = dfa.reference_model(n_changepoints=0)
+    else:
+        df = pd.DataFrame({"ds": pd.date_range("2017-01-01", periods=2), "y": [3.0, 5.0]})
+        m = dfa.reference_model()
+    m.fit(df)
+    assert list(m.changepoints_t) == [0.0] and m.params["delta"].shape == (1, 1)
+    assert len(m.changepoints) == 0
+    d = json.loads(serialize.model_to_json(m))
+    assert d["changepoints_t"] == [0.0] and np.shape(d["params"]["delta"]) == (1, 1)
+    rec = serialize.json_to_record(json.dumps(d), keys=[1, 1])
+    store = dfa.ParamsStore(str(tmp_path / case), config=m.config())
+    store.put_record(rec)
+    fut = m.make_future_dataframe(periods=10)
+    fc = m.predict(fut)
+    out = dfa.ForecastStoreItemModel(store).predict(None, fut.assign(store=1, item=1))
+    assert np.allclose(out["yhat"].to_numpy(np.float64), fc["yhat"].to_numpy(), rtol=1e-6, atol=1e-5)
+
+
+@pytest.mark.parametrize("mode", ["multiplicative", "additive"])
+def test_hessian_vs_oracle(golden_ref, mode):
+    """pf_hessian (the exact-MAP polish's model; FP64 MFMA tiles with per-row
+    quantities recomputed in the MFMA loop) equals the oracle's analytic
+    Hessian on the reference layout (P = 54), at the MAP and off it."""
+    from distributed_forecasting_amd.engine import ProphetConfig
+    c = ProphetConfig.reference()
+    c.seasonality_mode = mode
+    e = dfa.Engine(0, c)
+    ds, Y = golden_ref["ds_ns"], golden_ref["Y"][:4]
+    g = _grid(e, ds)
+    _, ys, th0, _, _ = e.prepare(g, _Y(g, Y))
+    rng = np.random.default_rng(11)
+    th = golden_ref["theta_map"][:4].copy()
+    th[2:, 2:27] += rng.normal(0, 0.01, (2, 25))
+    Hg = e.hessian(g, ys, torch.from_numpy(th).cuda()).cpu().numpy()
+    cfg = dict(po.DEFAULT_CONFIG, seasonality_mode=mode)
+    for s in range(4):
+        pb = po.build_problem(ds, Y[s], cfg).problem
+        Ho = so.hessian(pb, th[s])
+        assert np.max(np.abs(Hg[s] - Ho)) <= 1e-10 * np.max(np.abs(Ho)), s
+        assert np.array_equal(Hg[s], Hg[s].T)

@@ -238,3 +238,85 @@ def test_prophet_json_record_layout():
         serialize.json_to_record(json.dumps(bad))
     with pytest.raises(NotImplementedError, match="mcmc"):
         serialize.json_to_record(json.dumps(dict(d, mcmc_samples=10)))
+
+
+# ------------------------------------------------------------- params store
+def _json_model(mode="additive", growth="linear"):
+    import json
+    d = {"mcmc_samples": 0, "y_scale": 12.5, "start": 1356998400.0, "t_scale": 86400.0 * 1825,
+         "growth": growth, "seasonality_mode": mode, "interval_width": 0.95,
+         "changepoints_t": [0.1, 0.5],
+         "history_dates": pd.Series(pd.date_range("2013-01-01", periods=3), name="ds")
+         .to_json(orient="split", date_format="iso"),
+         "seasonalities": [["weekly"], {"weekly": {"period": 7, "fourier_order": 1,
+                                                   "prior_scale": 10.0, "mode": mode,
+                                                   "condition_name": None}}],
+         "extra_regressors": [[], {}],
+         "params": {"k": [[0.3]], "m": [[0.6]], "delta": [[0.01, -0.02]],
+                    "sigma_obs": [[0.05]], "beta": [[0.1, 0.2]]}}
+    return json.dumps(d)
+
+
+def test_params_store_refuses_other_config(tmp_path):
+    """an additive Prophet JSON imported into a store holding the
+    reference (multiplicative) config is refused, not served as multiplicative;
+    so is a different growth or interval width."""
+    from distributed_forecasting_amd import serialize
+    store = dfa.ParamsStore(str(tmp_path / "s"))          # reference config
+    with pytest.raises(ValueError, match="seasonality_mode"):
+        store.put_record(serialize.json_to_record(_json_model("additive"), keys=[1, 2]))
+    with pytest.raises(ValueError, match="growth"):
+        store.put_record(serialize.json_to_record(_json_model("multiplicative", "flat"), keys=[1, 2]))
+    ok = serialize.json_to_record(_json_model("multiplicative"), keys=[1, 2])
+    store.put_record(ok)
+    assert len(store) == 1
+    assert ok["series_id"][0] == B.series_id(np.array([[1, 2]]))[0]
+    bad = dict(ok, interval_width=np.float64(0.8))
+    with pytest.raises(ValueError, match="interval_width"):
+        store.put_record(bad)
+    with pytest.raises(ValueError, match="different ProphetConfig"):
+        dfa.ParamsStore(str(tmp_path / "s"), config=ProphetConfig())
+    d = __import__("json").loads(_json_model("multiplicative"))
+    d["seasonalities"][1]["weekly"]["mode"] = "additive"
+    with pytest.raises(NotImplementedError, match="own mode"):
+        serialize.json_to_record(__import__("json").dumps(d))
+
+
+def _writer(path, w, n):
+    import numpy as np
+    from distributed_forecasting_amd.serving import ParamsStore
+    st = ParamsStore(path, writer=f"w{w}")
+    for i in range(n):
+        st.put_record({"keys": np.array([[w, i]], np.int64), "theta": np.zeros((1, 3))})
+
+
+def test_params_store_concurrent_writers(tmp_path):
+    """several writers on one directory (torchrun ranks / Spark
+    executors) lose no record: names are unique per writer, the index is a
+    directory scan."""
+    import multiprocessing as mp
+    path = str(tmp_path / "shared")
+    dfa.ParamsStore(path)
+    ctx = mp.get_context("fork")
+    procs = [ctx.Process(target=_writer, args=(path, w, 12)) for w in range(4)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    st = dfa.ParamsStore(path)
+    assert len(st.record_names()) == 48
+    assert set(st.index()) == {(w, i) for w in range(4) for i in range(12)}
+    # a refit written later wins
+    st.put_record({"keys": np.array([[0, 0]], np.int64), "theta": np.ones((1, 3))})
+    name, row = st.index()[(0, 0)]
+    assert st.record(name)["theta"][row, 0] == 1.0
+
+
+def test_holiday_record_roundtrip():
+    from distributed_forecasting_amd import holidays as H
+    hd = H.synthetic_holidays([2016, 2017], n_per_year=3)
+    spec = H.holiday_spec(hd, 4.0, "additive")
+    rec = B.holiday_record(spec)
+    assert B.holiday_from_record(rec) == spec
+    assert B.holiday_from_record({}) is None and B.holiday_record(None) == {}
