@@ -216,7 +216,7 @@ class FittedBatch:
 
     @classmethod
     def fit_dense(cls, engine: E.Engine, fit_ds: np.ndarray, Y, history_dates=None,
-                  series_ids=None, polish: bool = True, seasons=None, cap=None,
+                  series_ids=None, polish: bool | None = None, seasons=None, cap=None,
                   holidays=None, priors=None) -> "FittedBatch":
         """Fit every row of Y ([n, T] numpy or device tensor, raw y) on the
         sorted date grid ``fit_ds`` (K1 grid + K2/K3 fit).  ``seasons``

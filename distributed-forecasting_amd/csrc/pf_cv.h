@@ -22,6 +22,104 @@ struct CvKArgs {
   double *metrics;
 };
 
+// k-th smallest (0-based) of n non-negative doubles by MSB-first radix
+// select on their bit patterns (monotone for x >= 0, +inf included): 8
+// passes of an 8-bit LDS histogram.  keys: LDS cache of the bits (n <= ncache)
+// or NULL to recompute from y / yh.  One wave; every lane returns the value.
+__device__ __forceinline__ double cv_radix_select(const unsigned long long *keys, int n, int k,
+                                                  const double *y, const float *yh, int *hist) {
+  const int lane = pf_lane();
+  unsigned long long prefix = 0ull, mask = 0ull;
+  for (int pass = 7; pass >= 0; --pass) {
+    const int sh = 8 * pass;
+    for (int b = lane; b < 256; b += 64) hist[b] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    for (int r = lane; r < n; r += 64) {
+      const unsigned long long key = keys ? keys[r]
+          : (unsigned long long)__double_as_longlong(fabs((y[r] - (double)yh[r]) / y[r]));
+      if ((key & mask) == prefix) atomicAdd(&hist[(int)((key >> sh) & 255ull)], 1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    int c[4], lsum = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { c[q] = hist[4 * lane + q]; lsum += c[q]; }
+    const double incl = wave_prefix_sum((double)lsum);
+    const double excl = incl - (double)lsum;
+    const unsigned long long hit = __ballot(incl > (double)k);
+    const int L = __ffsll((long long)hit) - 1;
+    int bsel = 0, below = 0;
+    if (lane == L) {
+      int acc = (int)excl;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (acc + c[q] > k) { bsel = 4 * lane + q; below = acc; break; }
+        acc += c[q];
+      }
+    }
+    bsel = __shfl(bsel, L, 64);
+    below = __shfl(below, L, 64);
+    prefix |= (unsigned long long)bsel << sh;
+    mask |= 255ull << sh;
+    k -= below;
+  }
+  return __longlong_as_double((long long)prefix);
+}
+
+// One horizon group holding every row (in-sample metrics: rolling_mean_by_h
+// with w = n is the plain mean, rolling_median_by_h the median): the 64
+// lanes stride over the rows and reduce; the MDAPE median comes from two
+// radix selects (ranks (n-1)/2 and n/2) over the APE bit patterns.
+__device__ __forceinline__ void cv_single_group(const CvKArgs &a, int series, const double *y,
+                                                const float *yh, const float *lo, const float *hi,
+                                                unsigned long long *cache, int ncache, int *hist) {
+  const int lane = pf_lane(), n = a.n_rows;
+  double se = 0.0, ae = 0.0, ape = 0.0, sape = 0.0, cov = 0.0, ymin = INFINITY;
+  for (int r = lane; r < n; r += 64) {
+    const double yv = y[r], fv = (double)yh[r];
+    const double e = yv - fv;
+    se = fma(e, e, se);
+    ae += fabs(e);
+    ape += fabs(e / yv);
+    sape += 2.0 * fabs(e) / (fabs(yv) + fabs(fv));
+    if (lo) cov += (yv >= (double)lo[r] && yv <= (double)hi[r]) ? 1.0 : 0.0;
+    ymin = fmin(ymin, fabs(yv));
+  }
+  se = wave_sum(se);
+  ae = wave_sum(ae);
+  ape = wave_sum(ape);
+  sape = wave_sum(sape);
+  cov = wave_sum(cov);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) ymin = fmin(ymin, __shfl_xor(ymin, o, 64));
+  bool bad = false;
+  const bool cached = n <= ncache;
+  for (int r = lane; r < n; r += 64) {
+    const double v = fabs((y[r] - (double)yh[r]) / y[r]);
+    bad |= (v != v);
+    if (cached) cache[r] = (unsigned long long)__double_as_longlong(v);
+  }
+  const bool anybad = __ballot(bad) != 0ull;
+  double v0 = NAN, v1 = NAN;
+  if (!anybad) {
+    v0 = cv_radix_select(cached ? cache : nullptr, n, (n - 1) / 2, y, yh, hist);
+    v1 = (n % 2) ? v0 : cv_radix_select(cached ? cache : nullptr, n, n / 2, y, yh, hist);
+  }
+  if (lane == 0) {
+    double *m = a.metrics + (size_t)series * PF_CV_NMETRICS;
+    const double w = (double)n;
+    const bool full = a.window <= n;   // a window larger than the rows yields nothing
+    m[PF_CV_MSE] = full ? se / w : NAN;
+    m[PF_CV_RMSE] = full ? sqrt(se / w) : NAN;
+    m[PF_CV_MAE] = full ? ae / w : NAN;
+    m[PF_CV_MAPE] = (full && ymin >= 1e-8) ? ape / w : NAN;
+    m[PF_CV_SMAPE] = full ? sape / w : NAN;
+    m[PF_CV_COVERAGE] = (full && lo) ? cov / w : NAN;
+    m[PF_CV_MDAPE] = (a.window <= n && !anybad) ? (v0 + v1) * 0.5 : NAN;
+  }
+}
+
 __global__ __launch_bounds__(64) void k_cv_metrics(CvKArgs a) {
   __shared__ double s_sum[PF_CV_MDAPE][PF_CV_GMAX];
   __shared__ int s_cnt[PF_CV_GMAX];
@@ -30,6 +128,11 @@ __global__ __launch_bounds__(64) void k_cv_metrics(CvKArgs a) {
   const float *yh = a.yhat + (size_t)series * a.n_rows;
   const float *lo = a.ylo ? a.ylo + (size_t)series * a.n_rows : nullptr;
   const float *hi = a.yhi ? a.yhi + (size_t)series * a.n_rows : nullptr;
+  if (a.n_groups == 1 && a.window == a.n_rows) {
+    cv_single_group(a, series, y, yh, lo, hi, reinterpret_cast<unsigned long long *>(&s_sum[0][0]),
+                    PF_CV_MDAPE * PF_CV_GMAX, s_cnt);
+    return;
+  }
   double ymin = INFINITY;
   for (int g = lane; g < a.n_groups; g += 64) {
     double se = 0.0, ae = 0.0, ape = 0.0, sape = 0.0, cov = 0.0;

@@ -50,6 +50,24 @@ __device__ __forceinline__ double pf_Ecol(int c, int s) {
   return (c == 0 || (c >= 2 && c - 2 < s)) ? 1.0 : 0.0;
 }
 
+// One k-step's MFMAs, tile Q..NT-1 (template recursion: every tile's block
+// pair is a compile-time constant, so the operand arrays stay in registers —
+// a runtime index would put them in scratch).
+template <int Q, int NB, int NT, int NBB>
+__device__ __forceinline__ void mfma_tiles(pf_d4 (&acc)[NT], const double (&lt)[2], const double (&rt)[2],
+                                           const double (&gt)[2], const double (&V)[NBB],
+                                           const double (&W)[NBB]) {
+  if constexpr (Q < NT) {
+    constexpr int bi = ptile_bi(Q, NB), bj = ptile_bj(Q, NB);
+    double A_, B_;
+    if constexpr (bj < 2) { A_ = lt[bi]; B_ = rt[bj]; }
+    else if constexpr (bi < 2) { A_ = gt[bi]; B_ = W[bj - 2]; }
+    else { A_ = V[bi - 2]; B_ = V[bj - 2]; }
+    acc[Q] = __builtin_amdgcn_mfma_f64_16x16x4f64(A_, B_, acc[Q], 0, 0, 0);
+    mfma_tiles<Q + 1, NB, NT, NBB>(acc, lt, rt, gt, V, W);
+  }
+}
+
 // Hessian of the smooth part at x, assembled into A = sm.U (stride LD, P
 // rows + 8 zero padding rows), damped by lam * max|diag| when lam > 0.
 // gh: smooth gradient at x (this lane's words).  Every thread calls it.
@@ -210,15 +228,7 @@ __device__ __forceinline__ void hessian_collective(const FitKArgs &a, FitSmem<NW
       W[b] = cu.X[b] * fma(u, kf, -r * smv[b]);
     }
     const double lt[2] = {wt * dzA, wt * dzB}, rt[2] = {dzA, dzB}, gt[2] = {gf * dzA, gf * dzB};
-#pragma unroll
-    for (int q = 0; q < NT; ++q) {
-      const int bi = ptile_bi(q, NB), bj = ptile_bj(q, NB);
-      double A_, B_;
-      if (bj < 2) { A_ = lt[bi]; B_ = rt[bj]; }
-      else if (bi < 2) { A_ = gt[bi]; B_ = W[bj - 2]; }
-      else { A_ = V[bi - 2]; B_ = V[bj - 2]; }
-      acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(A_, B_, acc[q], 0, 0, 0);
-    }
+    mfma_tiles<0, NB, NT, NBB>(acc, lt, rt, gt, V, W);
   }
   if constexpr (logistic) {
     if (c16 == 0 && rho_acc != 0.0) atomicAdd(&rho[cur_seg], rho_acc);

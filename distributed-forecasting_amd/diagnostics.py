@@ -106,3 +106,30 @@ def cv_metrics_batch(engine: E.Engine, fit_ds, Y, **kw) -> dict:
     """Host dict metric -> [n] numpy array (NaN where UPSTREAM skips)."""
     met = cv_metrics_device(engine, fit_ds, Y, **kw).cpu().numpy()
     return {name: met[:, i] for i, name in enumerate(L.CV_METRICS)}
+
+
+def insample_metrics(engine: E.Engine, y: torch.Tensor, yhat: torch.Tensor,
+                     yhat_lower: torch.Tensor | None = None,
+                     yhat_upper: torch.Tensor | None = None) -> torch.Tensor:
+    """[n, 7] float64 device tensor of K6's metric set over the history rows
+    (one horizon group, window = every row: the plain means, the median for
+    MDAPE; MAPE NaN where UPSTREAM skips it).  ``y`` [n, T] float64 and
+    ``yhat`` [n, >= T] float32 on the device; the per-series validation
+    metrics the multi-GPU path all-gathers (the reference logs its CV
+    metrics per series to MLflow, 02_training.py:187-192)."""
+    n, T = int(y.shape[0]), int(y.shape[1])
+    dev = y.device
+    yy = y.contiguous()
+    ff = yhat[:, :T].contiguous()
+    lo = yhat_lower[:, :T].contiguous() if yhat_lower is not None else None
+    hi = yhat_upper[:, :T].contiguous() if yhat_upper is not None else None
+    gs = torch.tensor([0, T], dtype=torch.int32, device=dev)
+    met = torch.empty((n, len(L.CV_METRICS)), dtype=torch.float64, device=dev)
+    a = L.PfCvArgs(n, T, 1, T, gs.data_ptr(), yy.data_ptr(), ff.data_ptr(),
+                   lo.data_ptr() if lo is not None else None,
+                   hi.data_ptr() if hi is not None else None, met.data_ptr())
+    rc = engine.ctx.lib.pf_cv_metrics(engine.ctx.h, ctypes.byref(a),
+                                      ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+    engine.ctx.check(rc, "pf_cv_metrics")
+    met._keep = (yy, ff, lo, hi, gs)
+    return met

@@ -24,6 +24,7 @@ from . import _lib as L
 from .holidays import HolidaySpec, holiday_columns
 
 NS_PER_DAY = 86400 * 10**9
+FIT_MODES = ("map", "stan_map", "stan")
 
 
 def pad_rows(T: int) -> int:
@@ -51,6 +52,22 @@ class ProphetConfig:
     # their interval endpoints — "exact" order statistics of the N draws (same
     # distribution, O(1) per row) or "sample" (materialise all N draws)
     interval_method: str = "exact"
+    # engine option: which optimum the fit returns (PyStan optimizing() at
+    # 02_training.py:172 stops where Stan's L-BFGS termination tests fire —
+    # 1e-6..2e-4 relative short of the MAP at the |delta| kink, at a point
+    # that moves with floating-point rounding):
+    #   "map"      Stan L-BFGS warm-up handed to the certified exact-MAP
+    #              polish (default; logistic growth runs Stan's full L-BFGS
+    #              first, see Engine.fit_opts);
+    #   "stan_map" Stan's full L-BFGS termination rules, then the polish (the
+    #              same certified MAP, reached from Stan's endpoint);
+    #   "stan"     Stan's full L-BFGS only: the reference-shaped answer
+    #              (status = Stan's termination code, no certificate).
+    fit_mode: str = "map"
+
+    def __post_init__(self):
+        if self.fit_mode not in FIT_MODES:
+            raise ValueError(f"fit_mode must be one of {FIT_MODES}")
 
     @classmethod
     def reference(cls) -> "ProphetConfig":
@@ -443,17 +460,24 @@ class Engine:
             setattr(o, k, v)
         return o
 
-    def fit(self, grid: DeviceGrid, Y: torch.Tensor, polish: bool = True,
-            stan_faithful: bool = False, cap: torch.Tensor | None = None, priors=None,
+    def fit(self, grid: DeviceGrid, Y: torch.Tensor, polish: bool | None = None,
+            stan_faithful: bool | None = None, cap: torch.Tensor | None = None, priors=None,
             **opt) -> FitResult:
         """Fit every row of Y [n, T_pad] (raw y, float64, on this GPU).
 
-        Default: Stan L-BFGS warm-up (<= lbfgs_warmup iterations) handed to
+        ``polish`` / ``stan_faithful`` default to the config's ``fit_mode``:
+        "map" = Stan L-BFGS warm-up (<= lbfgs_warmup iterations) handed to
         the exact-MAP polish (status PF_ST_MAP when certified; uncertified
-        series resume L-BFGS).  ``stan_faithful=True`` first runs Stan's full
-        termination rules (the reference's optimizer run), then polishes to
-        the same MAP; ``polish=False`` stops where Stan stops.  ``priors``
-        (``series_priors``) gives every row its own prior scales."""
+        series resume L-BFGS); "stan_map" (``stan_faithful=True``) first runs
+        Stan's full termination rules (the reference's optimizer run), then
+        polishes to the same MAP; "stan" (``polish=False``) stops where Stan
+        stops.  ``priors`` (``series_priors``) gives every row its own prior
+        scales."""
+        mode = self.config.fit_mode
+        if polish is None:
+            polish = mode != "stan"
+        if stan_faithful is None:
+            stan_faithful = mode == "stan_map"
         n = Y.shape[0]
         y_scale, y_scaled, theta, status, cap_scaled = self.prepare(grid, Y, cap)
         dev = Y.device

@@ -64,7 +64,8 @@ class Prophet:
                  daily_seasonality="auto", holidays=None, seasonality_mode="additive",
                  seasonality_prior_scale=10.0, holidays_prior_scale=10.0,
                  changepoint_prior_scale=0.05, mcmc_samples=0, interval_width=0.80,
-                 uncertainty_samples=1000, stan_backend=None, *, device=None, seed=0):
+                 uncertainty_samples=1000, stan_backend=None, *, device=None, seed=0,
+                 fit_mode="map"):
         if growth not in ("linear", "flat", "logistic"):
             raise ValueError('Parameter "growth" should be "linear", "logistic" or "flat".')
         if changepoints is not None:
@@ -98,6 +99,11 @@ class Prophet:
         self.device = device
         self.seed = seed
         self.stan_backend = stan_backend
+        if fit_mode not in E.FIT_MODES:
+            raise ValueError(f"fit_mode must be one of {E.FIT_MODES}")
+        # engine option (ProphetConfig.fit_mode): "map" (certified MAP),
+        # "stan_map", or "stan" (stop where Stan's L-BFGS stops)
+        self.fit_mode = fit_mode
         # set by fit
         self.history = None
         self.history_dates = None
@@ -123,7 +129,7 @@ class Prophet:
             holidays_prior_scale=self.holidays_prior_scale,
             changepoint_prior_scale=self.changepoint_prior_scale,
             interval_width=self.interval_width,
-            uncertainty_samples=int(self.uncertainty_samples or 0))
+            uncertainty_samples=int(self.uncertainty_samples or 0), fit_mode=self.fit_mode)
 
     # ---------------------------------------------------------------- fit
     def fit(self, df: pd.DataFrame, **kwargs) -> "Prophet":

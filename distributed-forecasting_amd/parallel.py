@@ -3,7 +3,11 @@ hash-sharded by splitmix64((store << 32) | item) mod world_size, no
 cross-GPU traffic until the final gather of forecasts / metrics.
 
 The reference's analogue is Spark's hashpartitioning(store, item) in front of
-``applyInPandas`` (notebooks/prophet/02_training.py:305-307).
+``applyInPandas`` (notebooks/prophet/02_training.py:305-307); the per-series
+validation metrics correspond to what ``train_model`` logs to MLflow
+(02_training.py:187-192).  Every exchange is a tensor collective
+(``all_gather_into_tensor``: RCCL over xGMI on GPUs, gloo on CPU), padded to
+the largest rank's row count; nothing is pickled.
 """
 from __future__ import annotations
 
@@ -26,30 +30,72 @@ def shard_indices(keys: np.ndarray, rank: int, world_size: int) -> np.ndarray:
     return np.flatnonzero(B.shard_of(keys, world_size) == rank)
 
 
+def gather_counts(n_local: int, device) -> list:
+    """Row count of every rank (one tiny all-gather)."""
+    ws = dist.get_world_size()
+    n = torch.tensor([int(n_local)], dtype=torch.int64, device=device)
+    cn = torch.zeros(ws, dtype=torch.int64, device=device)
+    dist.all_gather_into_tensor(cn, n)
+    return [int(c) for c in cn.tolist()]
+
+
 def gather_blocks(local: torch.Tensor, counts=None):
     """All-gather a per-rank [n_r, ...] block (padded to max n_r) over the
     default process group (RCCL on GPUs, gloo on CPU).  Returns (the
-    concatenation of every rank's valid rows, per-rank counts)."""
+    concatenation of every rank's valid rows, in rank order, per-rank counts)."""
     ws = dist.get_world_size()
-    n = torch.tensor([local.shape[0]], dtype=torch.int64, device=local.device)
     if counts is None:
-        cn = [torch.zeros_like(n) for _ in range(ws)]
-        dist.all_gather(cn, n)
-        counts = [int(c.item()) for c in cn]
+        counts = gather_counts(local.shape[0], local.device)
     mx = max(counts)
     pad = torch.zeros((mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
     pad[:local.shape[0]] = local
     out = torch.empty((ws * mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    dist.all_gather_into_tensor(out, pad)
+    dist.all_gather_into_tensor(out, pad.contiguous())
     parts = [out[r * mx:r * mx + counts[r]] for r in range(ws)]
     return torch.cat(parts, 0), counts
 
 
-def gather_frames(frame):
-    """Collect per-rank pandas frames on every rank (result assembly for the
-    pandas-level API; the bulk data path uses gather_blocks)."""
+def gather_results(keys: torch.Tensor, forecast: torch.Tensor, metrics: torch.Tensor | None = None,
+                   status: torch.Tensor | None = None, counts=None) -> dict:
+    """The engine's final exchange: every rank's
+    [S_g, k] int64 series keys, [S_g, 3, T] fp32 forecast blocks (yhat,
+    yhat_lower, yhat_upper), [S_g, M] fp64 validation metrics and [S_g]
+    int32 fit status, all-gathered to every rank.  One count exchange, then
+    one tensor all-gather per array."""
+    if counts is None:
+        counts = gather_counts(keys.shape[0], keys.device)
+    out = {"counts": counts}
+    out["keys"], _ = gather_blocks(keys, counts)
+    out["forecast"], _ = gather_blocks(forecast, counts)
+    if metrics is not None:
+        out["metrics"], _ = gather_blocks(metrics, counts)
+    if status is not None:
+        out["status"], _ = gather_blocks(status, counts)
+    return out
+
+
+def gather_frames(frame, key_cols=("store", "item"), device=None):
+    """Collect per-rank forecast frames ([ds, *keys, y, yhat, yhat_upper,
+    yhat_lower], the applyInPandas schema) on every rank with two tensor
+    all-gathers: an int64 block (ds in ns, keys) and a float32 block (the
+    value columns).  Returns the concatenated frame in rank order."""
     import pandas as pd
-    ws = dist.get_world_size()
-    objs = [None] * ws
-    dist.all_gather_object(objs, frame)
-    return pd.concat(objs, ignore_index=True)
+    key_cols = list(key_cols)
+    vcols = [c for c in frame.columns if c not in ["ds"] + key_cols]
+    dev = torch.device("cpu") if device is None else device
+    ints = np.column_stack([frame["ds"].to_numpy("datetime64[ns]").astype(np.int64)] +
+                           [frame[k].to_numpy(np.int64) for k in key_cols]) if len(frame) else \
+        np.zeros((0, 1 + len(key_cols)), np.int64)
+    vals = frame[vcols].to_numpy(np.float32) if len(frame) else np.zeros((0, len(vcols)), np.float32)
+    it = torch.from_numpy(np.ascontiguousarray(ints)).to(dev)
+    vt = torch.from_numpy(np.ascontiguousarray(vals)).to(dev)
+    counts = gather_counts(it.shape[0], dev)
+    gi, _ = gather_blocks(it, counts)
+    gv, _ = gather_blocks(vt, counts)
+    gi, gv = gi.cpu().numpy(), gv.cpu().numpy()
+    out = {"ds": gi[:, 0].astype("datetime64[ns]")}
+    for j, k in enumerate(key_cols):
+        out[k] = gi[:, 1 + j].astype(frame[k].dtype if len(frame) else np.int32)
+    for j, c in enumerate(vcols):
+        out[c] = gv[:, j]
+    return pd.DataFrame(out)[list(frame.columns)]

@@ -14,6 +14,11 @@ Writes (all plain arrays / JSON, no pickles):
                         KAT, Stan-phase fit and the oracle's certified MAP
                         (Stan's full L-BFGS + damped exact-MAP polish), and the
                         warm-up(60) + polish basin check
+  golden_stan64.npz     64 fresh daily series (config_index 2): the oracle's
+                        Stan-phase endpoint (the reference-shaped answer that
+                        fit_mode="stan" is pinned against), the same run from
+                        an init perturbed by 1e-14 (Stan's own rounding
+                        sensitivity) and the certified MAP
   bench_manifest.json   E = the oracle's Stan-faithful objective+gradient
                         evaluation count for each of the 500 bench series
                         (roofline.achieved is computed from E)
@@ -155,6 +160,27 @@ def configs4_fixture(n=8):
     np.savez_compressed(os.path.join(OUT, "golden_configs4.npz"), **out)
 
 
+def _stan64_one(s):
+    ds = synthetic.daily_dates()
+    y = synthetic.sales_matrix(64, ds, config_index=2)[s]
+    st = po.build_problem(ds, y)
+    th, f, status, it, ne = so.fit_setup(st)
+    th0 = st.theta0.copy()
+    th0[0] *= 1.0 + 1e-14
+    thp, fp, *_ = so.lbfgs(st.problem, th0)
+    thm, fm, *_ = so.fit_map(st)
+    return th, f, status, thp, fp, thm, fm
+
+
+def stan64_fixture():
+    with Pool(min(8, os.cpu_count() or 1)) as pool:
+        res = pool.map(_stan64_one, range(64))
+    keys = ["theta_stan", "f_stan", "status_stan", "theta_stan_perturbed", "f_stan_perturbed",
+            "theta_map", "f_map"]
+    out = {k: np.array([r[i] for r in res]) for i, k in enumerate(keys)}
+    np.savez_compressed(os.path.join(OUT, "golden_stan64.npz"), **out)
+
+
 def bench_manifest(n=500):
     ds = synthetic.daily_dates()
     Y = synthetic.sales_matrix(n, ds)
@@ -178,7 +204,7 @@ def _stan_evals(args):
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["reference", "edge", "bench", "configs4"]
+    which = sys.argv[1:] or ["reference", "edge", "bench", "configs4", "stan64"]
     if "reference" in which:
         reference_fixture()
     if "edge" in which:
@@ -187,3 +213,5 @@ if __name__ == "__main__":
         bench_manifest()
     if "configs4" in which:
         configs4_fixture()
+    if "stan64" in which:
+        stan64_fixture()

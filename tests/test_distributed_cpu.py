@@ -54,3 +54,79 @@ def test_gloo_world2_shard_and_gather():
         assert rows.shape == (500, 3)
         assert np.array_equal(rows[:, 2], rows[:, 0] * 1000 + rows[:, 1])
         assert len({(a, b) for a, b in rows[:, :2].astype(int)}) == 500
+
+
+TF = 1916   # 1826 history + 90 forecast rows (configs[1] forecast block)
+
+
+def _series_outputs(keys):
+    """Deterministic stand-in for one rank's engine outputs with the real
+    shapes: [n, 3, TF] fp32 forecast blocks, [n, 4] fp64 validation metrics
+    (mse, rmse, mae, mape), [n] int32 status — each a function of the series
+    key only, as the engine's are (per-series RNG stream, independent fits)."""
+    k = keys.astype(np.float64)
+    t = np.arange(TF)[None, :]
+    base = (k[:, :1] * 7.0 + k[:, 1:2]) * (1.0 + 0.01 * np.sin(t / (5.0 + k[:, 1:2])))
+    fc = np.stack([base, base - 1.5, base + 1.5], 1).astype(np.float32)
+    met = np.column_stack([k[:, 0] ** 2 + k[:, 1], k[:, 0] + 0.5, k[:, 1] / 3.0, 1.0 / (k[:, 0] + k[:, 1])])
+    st = (70 + (keys[:, 0] % 2)).astype(np.int32)
+    return fc, met, st
+
+
+def _frame(keys, fc):
+    import pandas as pd
+    ds = (np.datetime64("2013-01-01", "ns") + np.arange(TF) * np.timedelta64(1, "D"))
+    n = len(keys)
+    return pd.DataFrame({"ds": np.tile(ds, n), "store": np.repeat(keys[:, 0], TF).astype(np.int32),
+                         "item": np.repeat(keys[:, 1], TF).astype(np.int32),
+                         "y": np.float32(1.0),
+                         "yhat": fc[:, 0].reshape(-1), "yhat_upper": fc[:, 2].reshape(-1),
+                         "yhat_lower": fc[:, 1].reshape(-1)})
+
+
+def _worker_results(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        keys = np.stack(np.meshgrid(np.arange(1, 11), np.arange(1, 51), indexing="ij"), -1).reshape(-1, 2)
+        mine = parallel.shard_indices(keys, rank, world)
+        fc, met, st = _series_outputs(keys[mine])
+        g = parallel.gather_results(torch.from_numpy(keys[mine].astype(np.int64)), torch.from_numpy(fc),
+                                    torch.from_numpy(met), torch.from_numpy(st))
+        fr = parallel.gather_frames(_frame(keys[mine], fc))
+        q.put((rank, g["counts"], g["keys"].numpy(), g["forecast"].numpy(), g["metrics"].numpy(),
+               g["status"].numpy(), fr))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_gathers_real_shapes_equal_world1():
+    """The N>1 exchange on the engine's real shapes: per-rank [S_g, 3, 1916]
+    fp32 forecast blocks, [S_g, 4] fp64 metrics, [S_g] int32 status and the
+    applyInPandas-schema frame, all-gathered as tensors over gloo (RCCL on
+    the GPUs) — equal, series by series, to the world-1 output."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_results, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(2)]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    keys = np.stack(np.meshgrid(np.arange(1, 11), np.arange(1, 51), indexing="ij"), -1).reshape(-1, 2)
+    fc1, met1, st1 = _series_outputs(keys)          # world-1 output
+    ref = {tuple(k): i for i, k in enumerate(keys.tolist())}
+    fr1 = _frame(keys, fc1).sort_values(["store", "item", "ds"]).reset_index(drop=True)
+    for rank, counts, gk, gf, gm, gs, fr in res:
+        assert sum(counts) == 500 and len(counts) == 2
+        assert gf.shape == (500, 3, TF) and gf.dtype == np.float32
+        assert gm.shape == (500, 4) and gm.dtype == np.float64 and gs.dtype == np.int32
+        idx = np.array([ref[tuple(k)] for k in gk.tolist()])
+        assert sorted(idx.tolist()) == list(range(500))
+        assert np.array_equal(gf, fc1[idx]) and np.array_equal(gm, met1[idx]) and np.array_equal(gs, st1[idx])
+        frs = fr.sort_values(["store", "item", "ds"]).reset_index(drop=True)
+        assert list(frs.columns) == list(fr1.columns)
+        assert frs.dtypes.equals(fr1.dtypes)
+        assert frs.equals(fr1)

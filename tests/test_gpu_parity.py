@@ -631,3 +631,79 @@ def test_hessian_vs_oracle(golden_ref, mode):
         Ho = so.hessian(pb, th[s])
         assert np.max(np.abs(Hg[s] - Ho)) <= 1e-10 * np.max(np.abs(Ho)), s
         assert np.array_equal(Hg[s], Hg[s].T)
+
+
+def _yhat_dist(ds, Y, th_a, th_b):
+    fut = po.make_future_dates(ds, 90)
+    out = []
+    for s in range(Y.shape[0]):
+        st = po.build_problem(ds, Y[s])
+        ya = po.predict_point(st, po.params_from_theta(th_a[s], st.problem.S), fut)["yhat"]
+        yb = po.predict_point(st, po.params_from_theta(th_b[s], st.problem.S), fut)["yhat"]
+        out.append(np.abs(ya - yb).max() / st.hist.y_scale)
+    return np.array(out)
+
+
+def test_stan_mode_is_reference_shaped(golden_ref):
+    """fit_mode="stan" (Stan's L-BFGS termination rules, no polish) returns
+    the reference-shaped answer (PyStan optimizing, 02_training.py:172;
+    forecast 02_training.py:201-205), pinned against the oracle's Stan-phase
+    endpoint on golden_reference.npz (8 series) and golden_stan64.npz (64
+    fresh series).  Stan's endpoint is itself only defined up to its own
+    rounding sensitivity: the oracle restarted from an init perturbed by
+    1e-14 (golden_stan64 theta_stan_perturbed) moves by up to ~3e-3 y_scale,
+    more than 1e-3 for ~4-6 % of series (bench.py accuracy, 500 series), so
+    the 1e-3 bar is distributional.  Bar: the objective within Stan's stall
+    band; max|dyhat|/y_scale <= 1e-3 on >= 90 % of the series and <= 5e-3 on
+    all; the fraction above 1e-3 no larger than the oracle's own
+    perturbation fraction + 5 %."""
+    import os
+    from distributed_forecasting_amd.engine import ProphetConfig
+    c = ProphetConfig.reference()
+    c.fit_mode = "stan"
+    e = dfa.Engine(0, c)
+    ds = synthetic.daily_dates()
+    with np.load(os.path.join(os.path.dirname(__file__), "golden", "golden_stan64.npz")) as z:
+        g64 = {k: z[k] for k in z.files}
+    Y64 = synthetic.sales_matrix(64, ds, config_index=2)
+    floor = _yhat_dist(ds, Y64, g64["theta_stan"], g64["theta_stan_perturbed"])
+    for Y, th_o, f_o, fl in ((golden_ref["Y"], golden_ref["theta_stan"], golden_ref["f_stan"], None),
+                             (Y64, g64["theta_stan"], g64["f_stan"], floor)):
+        g = _grid(e, ds)
+        fit = e.fit(g, _Y(g, Y))
+        st = fit.status.cpu().numpy()
+        assert np.all(np.isin(st, [0, 10, 20, 21, 30, 31])), st      # Stan's own termination codes
+        f = fit.f.cpu().numpy()
+        assert np.all(np.abs(f - f_o) <= 2e-4 * np.abs(f_o))          # Stan's stall band
+        d = _yhat_dist(ds, Y, fit.theta.cpu().numpy(), th_o)
+        assert np.all(d <= 5e-3), d.max()
+        assert np.mean(d <= 1e-3) >= 0.9, d
+        if fl is not None:
+            assert np.mean(d > 1e-3) <= np.mean(fl > 1e-3) + 0.05, (np.mean(d > 1e-3), np.mean(fl > 1e-3))
+
+
+@pytest.mark.parametrize("n", [1826, 1825, 5000])
+def test_cv_metrics_single_group_insample(eng, n):
+    """K6's one-group path (in-sample validation metrics: window = every
+    row; the N>1 path all-gathers them): means, and MDAPE by radix select
+    (LDS-cached keys for n <= 3072, recomputed beyond), equal to the
+    oracle's UPSTREAM performance_metrics with rolling_window = 1."""
+    import ctypes
+    from distributed_forecasting_amd import _lib as L, diagnostics
+    rng = np.random.default_rng(n)
+    y = rng.uniform(1, 50, (3, n))
+    y[1, ::9] = np.round(y[1, ::9])
+    f = (y + rng.normal(0, 3, y.shape)).astype(np.float32)
+    f[2, ::5] = y[2, ::5].astype(np.float32)              # ties
+    lo, hi = f - 3, f + 3
+    met = diagnostics.insample_metrics(eng, torch.from_numpy(y).cuda(), torch.from_numpy(f).cuda(),
+                                       torch.from_numpy(lo).cuda(), torch.from_numpy(hi).cuda())
+    torch.cuda.synchronize()
+    m = met.cpu().numpy()
+    h = np.ones(n)
+    for s in range(3):
+        pm = po.performance_metrics(y[s], f[s].astype(np.float64), h, rolling_window=1.0,
+                                    metrics=tuple(L.CV_METRICS), yhat_lower=lo[s], yhat_upper=hi[s])
+        for j, k in enumerate(L.CV_METRICS):
+            want = float(np.mean(pm[k]))
+            assert abs(m[s, j] - want) <= 1e-12 * max(1.0, abs(want)), (n, s, k, m[s, j], want)

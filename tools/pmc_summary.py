@@ -35,7 +35,7 @@ def main(src, tag):
         for row in csv.DictReader(f):
             out[row["Name"]]["avg_ns"] = float(row["AverageNs"])
             out[row["Name"]]["calls"] = int(row["Calls"])
-    for sub in ("pmc_fetch", "pmc_write", "pmc_sq"):
+    for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_mfma"):
         p = os.path.join(src, sub, "run_counter_collection.csv")
         if not os.path.exists(p):
             continue
@@ -52,6 +52,14 @@ def main(src, tag):
             d["frac_wait_any"] = d.get("SQ_WAIT_ANY", 0) / w
             d["frac_wait_inst_any"] = d.get("SQ_WAIT_INST_ANY", 0) / w
             d["frac_active_inst_any"] = d.get("SQ_ACTIVE_INST_ANY", 0) / w
+            if "SQ_ACTIVE_INST_VALU" in d:
+                # ACTIVE_INST_* and WAVE_CYCLES are both quad-cycle counts
+                d["frac_active_inst_valu"] = d["SQ_ACTIVE_INST_VALU"] / w
+        if "SQ_INSTS_VALU_MFMA_MOPS_F64" in d:
+            # one MOP = 512 FLOP (gfx9 MFMA MOPS unit); 16x16x4 f64 = 2048 FLOP = 4 MOPS
+            d["mfma_f64_flops_per_launch"] = 512.0 * d["SQ_INSTS_VALU_MFMA_MOPS_F64"]
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in d and d.get("SQ_BUSY_CU_CYCLES", 0) > 0:
+            d["mfma_busy_per_cu_busy"] = d["SQ_VALU_MFMA_BUSY_CYCLES"] / d["SQ_BUSY_CU_CYCLES"]
     with open(os.path.join(prof, f"{tag}_pmc.json"), "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
     kf = "k_fit_polish" if "k_fit_polish" in out else "k_fit"
