@@ -13,6 +13,7 @@ DEPS = SOURCES + [os.path.join(_HERE, "csrc", "pf_common.h"),
                   os.path.join(_HERE, "csrc", "pf_cv.h"),
                   os.path.join(_HERE, "csrc", "pf_ostat.h"),
                   os.path.join(_HERE, "csrc", "pf_mc.h"),
+                  os.path.join(_HERE, "csrc", "pf_tile.h"),
                   os.path.join(_ROOT, "include", "prophet_hip.h")]
 OUT = os.path.join(_HERE, "libprophet_hip.so")
 ARCH = os.environ.get("PF_OFFLOAD_ARCH", "gfx950")

@@ -1455,6 +1455,7 @@ __device__ __forceinline__ bool lbfgs_advance(const pf_fit_opts &o, LbLds<PW> &L
 
 
 #include "pf_polish.h"
+#include "pf_tile.h"
 
 // ---------------------------------------------------------------- K3 kernel
 // pass 0: first L-BFGS run; pass > 0: resume the series the polish did not
@@ -1939,6 +1940,7 @@ void pf_default_fit_opts(pf_fit_opts *o) {
   o->polish_max_iter = 50;  // accepted Newton steps (damped logistic fits from far away need ~30)
   o->lbfgs_warmup = 60;
   o->lbfgs_warmup_evals = 0;
+  o->tile_min_series = 2048;
 }
 
 int pf_num_changepoints(int T, int n_changepoints, double changepoint_range) {
@@ -2110,7 +2112,18 @@ int launch_fitlike(pf_ctx *ctx, int what, const FitKArgs &a, int n, hipStream_t 
     } else {
       caps[0] = a.o.max_iter; warm[0] = 0;
     }
-    if (npass == 3 && !getenv_flag("PF_SPLIT_POLISH")) {
+    // tiled first pass (K3T, 16 series per workgroup, MFMA row pass) for
+    // large batches of the layouts it covers; the per-series kernels finish
+    constexpr bool TILE_OK = (MODE & (PF_MODE_LOGI | PF_MODE_WIDE)) == 0 && KMAX <= 32;
+    bool tile = false;
+    size_t smem_t = 0;
+    if constexpr (TILE_OK) {
+      smem_t = TileSmem<MODE>::bytes(a.P);
+      tile = a.o.tile_min_series >= 0 && n >= a.o.tile_min_series && a.P <= 60 && a.K <= 32 &&
+             a.S + 1 <= 32 && a.growth != PF_GROWTH_LOGISTIC && !a.tau_series && !a.sigmas_series &&
+             smem_t <= 160 * 1024;
+    }
+    if (npass == 3 && !tile && !getenv_flag("PF_SPLIT_POLISH")) {
       if constexpr (HAS_POLISH) {
         auto kfp = k_fit_polish<NW, KMAX, O0, O1, O2, MODE>;
         PF_HIP(ctx, hipFuncSetAttribute((const void *)kfp, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2128,8 +2141,18 @@ int launch_fitlike(pf_ctx *ctx, int what, const FitKArgs &a, int n, hipStream_t 
       if (!warm[ps]) b.o.lbfgs_warmup_evals = 0;
       b.pass = ps;
       const int v = ps == 0 ? 0 : 1;
-      PF_TIMED_LAUNCH(ctx, v ? "k_fit_resume" : "k_fit", n, st, kf[v], dim3(n), dim3(NW * 64),
-                      smem, st, b);
+      if (ps == 0 && tile) {
+        if constexpr (TILE_OK) {
+          auto kt = k_fit_tile<MODE>;
+          PF_HIP(ctx, hipFuncSetAttribute((const void *)kt, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)smem_t));
+          const int nt = (n + PF_TS - 1) / PF_TS;
+          PF_TIMED_LAUNCH(ctx, "k_fit_tile", nt, st, kt, dim3(nt), dim3(PF_TNW * 64), smem_t, st, b, n);
+        }
+      } else {
+        PF_TIMED_LAUNCH(ctx, v ? "k_fit_resume" : "k_fit", n, st, kf[v], dim3(n), dim3(NW * 64),
+                        smem, st, b);
+      }
       PF_HIP(ctx, hipGetLastError());
       if (polish) {
         PF_TIMED_LAUNCH(ctx, v ? "k_polish_resume" : "k_polish", n, st, kpl[v], dim3(n),

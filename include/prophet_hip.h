@@ -107,6 +107,11 @@ typedef struct {
    * also ends a warm-up pass once it has used that many evaluations (at the
    * next accepted iterate).                                                  */
   int32_t lbfgs_warmup, lbfgs_warmup_evals;
+  /* engine: batches of at least tile_min_series series run the first L-BFGS
+   * pass in the tiled kernel (16 series per workgroup, FP64 MFMA row pass,
+   * per-series lane-quad L-BFGS) when the layout allows it (linear / flat
+   * growth, P <= 60, K <= 32, shared prior scales); < 0 never.            */
+  int32_t tile_min_series;
 } pf_fit_opts;
 
 /* component blocks pf_predict can report (seasonalities, holidays, ...) */

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("n", type=int, nargs="?", default=None)
     ap.add_argument("--chunk", type=int, default=None)
     ap.add_argument("--method", default=None, help="interval method (default per config)")
+    ap.add_argument("--tile-min", type=int, default=None,
+                    help="pf_fit_opts.tile_min_series (default: the engine's, 2048; -1 disables K3T)")
     args = ap.parse_args()
     import torch
     import distributed_forecasting_amd as dfa
@@ -88,7 +90,8 @@ def main():
     sid = [torch.arange(a, b, dtype=torch.int32, device=dev) for a, b in chunks]
 
     def run(k):
-        fit = eng.fit(grid, Yd[k], cap=None if capd is None else capd[k])
+        kw = {} if args.tile_min is None else {"tile_min_series": args.tile_min}
+        fit = eng.fit(grid, Yd[k], cap=None if capd is None else capd[k], **kw)
         fg = eng.predict_grid(fit, fut)
         cf = None
         if capd is not None:
@@ -113,7 +116,7 @@ def main():
     eng.ctx.set_timing(False)
     res = {"metric": "series fit+forecast/sec", "config_index": args.config, "value": n / el,
            "unit": "series/s", "n_gpus": 1, "seconds": el, "workload": work, "chunk": chunk,
-           "kernels_ms_total": kern,
+           "kernels_ms_total": kern, "tile_min_series": args.tile_min,
            "n_eval_mean": float(np.mean([s[0] for s in stats])),
            "map_certified": float(np.mean([s[1] for s in stats])),
            "data": "synthetic (SURVEY.md §8d generators)"}

@@ -1,0 +1,37 @@
+"""Diagnostic: per-phase cycles per evaluation of the tiled fit kernel K3T
+(block 0, wave 0 lane 0 s_memtime sums; -DPF_STAMPS build, never the product).
+    python tools/stamps_tile.py [n]"""
+import ctypes, os, subprocess, sys, time
+import numpy as np, torch
+sys.path.insert(0, ".")
+here = "distributed-forecasting_amd"
+out = os.path.join(here, "libprophet_hip_stamps.so")
+if not os.path.exists(out):
+    subprocess.check_call(["sh", "tools/build_stamps.sh"])
+from distributed_forecasting_amd import _lib
+_lib.load(os.path.abspath(out))
+import distributed_forecasting_amd as dfa
+from distributed_forecasting_amd import synthetic
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+ds = synthetic.daily_dates(); Y = synthetic.sales_matrix(n, ds, config_index=2)
+eng = dfa.Engine(0)
+seasons = eng.config.seasons(int(ds[0]), int(ds[-1]), int(ds[1] - ds[0]))
+grid = dfa.build_grid(ds, seasons, start_ns=int(ds[0]), t_scale_ns=int(ds[-1] - ds[0]))
+Yd = torch.zeros((n, grid.T_pad), dtype=torch.float64, device="cuda"); Yd[:, :grid.T] = torch.from_numpy(Y).cuda()
+lib = _lib._lib
+buf = (ctypes.c_ulonglong * 32)()
+eng.fit(grid, Yd, polish=False, tile_min_series=1); torch.cuda.synchronize()
+lib.pf_debug_stamps(buf, 1)
+t0 = time.time()
+fit = eng.fit(grid, Yd, polish=False, tile_min_series=1, lbfgs_warmup=0); torch.cuda.synchronize()
+dt = time.time() - t0
+lib.pf_debug_stamps(buf, 1)
+v = np.array(list(buf), dtype=np.float64)
+ne = max(v[7], 1)
+ph = {"row pass (wave 0)": v[1] - v[0], "barrier wait": v[2] - v[1], "assemble": v[3] - v[2],
+      "lbfgs step": v[4] - v[3], "publish+zero": v[5] - v[4], "end barrier": v[6] - v[5]}
+print(f"n={n} fit(polish=False) {dt*1e3:.1f} ms; tile 0: {ne:.0f} evaluations; "
+      f"series0 n_eval={fit.n_eval[0].item()}")
+tot = sum(ph.values())
+for k, c in ph.items():
+    print(f"   {k:20s} {c / ne:9.0f} cycles/eval {100 * c / tot:5.1f}%")
