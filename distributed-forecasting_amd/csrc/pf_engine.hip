@@ -342,6 +342,9 @@ struct FitKArgs {
   int R, TQ;                 // rows per thread, TQ = NL*R
   const double *tP, *XTP;    // [TQ], [K][TQ]
   const int32_t *sgP;        // [TQ] seg | (#changepoints first active at this row) << 16
+  // row-major copy of the features for the tiled kernel K3T: [Tp][32],
+  // features >= K zero (NULL unless the tiled path may run)
+  const double *XR;
   const double *sigmas, *s_a, *s_m;
   double tau;
   // hyperparameter batching: per-series prior scales (NULL: the shared
@@ -2031,6 +2034,15 @@ __global__ __launch_bounds__(256) void k_permute_grid(const double *__restrict__
   for (int f = 0; f < K; ++f) XTP[(size_t)f * TQ + q] = v ? XT[(size_t)f * Tp + i] : 0.0;
 }
 
+// Row-major feature copy for K3T: XR[r][f] = X[r][f] (f < K), 0 for K <= f < 32.
+__global__ __launch_bounds__(256) void k_grid_rowmajor(const double *__restrict__ XT, int Tp, int K,
+                                                       double *__restrict__ XR) {
+  const size_t q = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (q >= (size_t)Tp * 32) return;
+  const int r = (int)(q >> 5), f = (int)(q & 31);
+  XR[q] = f < K ? XT[(size_t)f * Tp + r] : 0.0;
+}
+
 // ---------------------------------------------------------------- dispatch
 #define PF_FIT_NW 4
 namespace {
@@ -2118,9 +2130,9 @@ int launch_fitlike(pf_ctx *ctx, int what, const FitKArgs &a, int n, hipStream_t 
     bool tile = false;
     size_t smem_t = 0;
     if constexpr (TILE_OK) {
-      smem_t = TileSmem<MODE>::bytes(a.P);
-      tile = a.o.tile_min_series >= 0 && n >= a.o.tile_min_series && a.P <= 60 && a.K <= 32 &&
-             a.S + 1 <= 32 && a.growth != PF_GROWTH_LOGISTIC && !a.tau_series && !a.sigmas_series &&
+      smem_t = TileSmem<MODE>::bytes();
+      tile = a.o.tile_min_series >= 0 && n >= a.o.tile_min_series && a.P <= PF_TV && a.K <= 32 &&
+             a.S + 1 <= 32 && a.growth != PF_GROWTH_LOGISTIC && !a.tau_series && !a.sigmas_series && a.XR &&
              smem_t <= 160 * 1024;
     }
     if (npass == 3 && !tile && !getenv_flag("PF_SPLIT_POLISH")) {
@@ -2221,23 +2233,33 @@ extern "C" {
 
 // Context scratch for one fit-like call: [lane-blocked grid | polish rows],
 // then the permutation launch (stream-ordered with the fit that reads it).
-static int prepare_fit_scratch(pf_ctx *ctx, FitKArgs &a, hipStream_t st) {
+static int prepare_fit_scratch(pf_ctx *ctx, FitKArgs &a, hipStream_t st, bool rowmajor = false) {
   const size_t TQ = (size_t)a.TQ;
   size_t gbytes = TQ * sizeof(double) * (1 + (size_t)a.K) + TQ * sizeof(int32_t);
   gbytes = (gbytes + 255) & ~(size_t)255;
+  const size_t rbytes = rowmajor ? (size_t)a.Tp * 32 * sizeof(double) : 0;
   void *w = nullptr;
-  const int rc = ctx_workspace(ctx, gbytes, &w);
+  const int rc = ctx_workspace(ctx, gbytes + rbytes, &w);
   if (rc) return rc;
   double *base = (double *)w;
   a.tP = base;
   a.XTP = base + TQ;
   a.sgP = (int32_t *)(base + TQ * (1 + (size_t)a.K));
+  a.XR = nullptr;
   const int nb = (int)((TQ + 255) / 256);
   PF_TIMED_LAUNCH(ctx, "k_permute_grid", nb, st, k_permute_grid, dim3(nb), dim3(256), 0, st,
                   a.t, a.seg, a.XT, a.T, a.Tp, a.K, a.S, a.R, PF_FIT_NW * 64,
                   const_cast<double *>(a.tP), const_cast<int32_t *>(a.sgP),
                   const_cast<double *>(a.XTP));
   PF_HIP(ctx, hipGetLastError());
+  if (rowmajor) {
+    double *xr = (double *)((char *)w + gbytes);
+    const int nr = (int)(((size_t)a.Tp * 32 + 255) / 256);
+    PF_TIMED_LAUNCH(ctx, "k_grid_rowmajor", nr, st, k_grid_rowmajor, dim3(nr), dim3(256), 0, st,
+                    a.XT, a.Tp, a.K, xr);
+    PF_HIP(ctx, hipGetLastError());
+    a.XR = xr;
+  }
   return 0;
 }
 
@@ -2290,7 +2312,10 @@ int pf_fit(pf_ctx *ctx, const pf_problem *pb, const pf_fit_opts *opts, double *t
   a.n_iter = n_iter;
   a.n_eval = n_eval;
   a.o = *opts;
-  rc = prepare_fit_scratch(ctx, a, (hipStream_t)stream);
+  // the tiled first pass reads a row-major feature copy
+  const bool maybe_tile = opts->tile_min_series >= 0 && pb->n_series >= opts->tile_min_series &&
+                          pb->grid.K <= 32;
+  rc = prepare_fit_scratch(ctx, a, (hipStream_t)stream, maybe_tile);
   if (rc) return rc;
   return dispatch_fitlike(ctx, PF_LAUNCH_FIT, a, pb->n_series, pb->fourier_orders, mode_of(pb),
                           (hipStream_t)stream);

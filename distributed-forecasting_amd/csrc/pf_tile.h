@@ -7,29 +7,39 @@
 // matrix cores:
 //   X[T x K] . B[K x 16]  (B = beta o s_m per series)       -> Xb, C layout
 //   X'[K x T] . W[T x 16] (W = r o trend per series)        -> beta gradient
-// both v_mfma_f64_16x16x4f64 over 16-row chunks (the first product's
-// accumulator registers are the second product's B operand: the C layout's
-// rows are the next MFMA's k index).  The changepoint contraction A[T x C]
-// . Delta[C x 16] is a step matrix: the trend reads per-series segment
-// tables (k_s, m_s) — the exact contraction at O(1) per element — and its
-// adjoint is a segment sum of G = r(1 + Xb_m), G t per series.
-// Residuals, likelihood and prior terms are elementwise in the C layout.
+// both v_mfma_f64_16x16x4f64 over 16-row chunks (the C layout's rows are
+// the second product's k index, so the elementwise results feed it from
+// registers).  The changepoint contraction A[T x C] . Delta[C x 16] is a
+// step matrix: the trend reads per-series segment tables (k_s, m_s) — the
+// exact contraction at O(1) per element — and its adjoint is a segment sum
+// of G = r(1 + Xb_m), G t per series.  Residuals, likelihood and prior terms
+// are elementwise in the C layout.
 //
-// L-BFGS: each series owns a lane quad of wave 0 (16 parameters per lane,
-// p = q + 4i) running Stan 2.19's BFGSMinimizer<LBFGSUpdate> + Wolfe line
-// search (same control flow as oracle/stan_lbfgs.c, two-loop recursion),
-// with per-series convergence masking: a series that terminates stops
-// moving and the tile exits when all 16 have.  State lives in LDS.
+// Row pass: each wave takes a contiguous quarter of the 16-row chunks,
+// software-pipelined — the Xb MFMAs of chunk c+1 are issued before chunk c's
+// elementwise VALU work (matrix and vector pipes overlap within the wave),
+// and global loads run two chunks ahead (one wave per SIMD: nothing else
+// hides L2 / HBM latency).
 //
-// Scope: linear / flat growth, P = 3 + S + K <= 60, shared prior scales
-// (the reference layout and the fallback-free configs[2]/[3] shapes); the
-// per-series kernel K3 covers the rest.  The exact-MAP polish runs after it
-// (k_polish, one workgroup per series).
+// L-BFGS: every series owns 16 lanes (4 series per wave, all 4 waves busy;
+// parameter p = g + 16 i in lane g) running Stan 2.19's
+// BFGSMinimizer<LBFGSUpdate> + Wolfe line search (same control flow as
+// oracle/stan_lbfgs.c, two-loop recursion), with per-series convergence
+// masking: a series that terminates stops moving and the tile exits when
+// all 16 have.  State lives in LDS between evaluations.
+//
+// Scope: linear / flat growth, P = 3 + S + K <= 64, K <= 32, S + 1 <= 32,
+// shared prior scales (the reference layout and the configs[2]/[3]
+// shapes); the per-series kernel K3 covers the rest.  The exact-MAP polish
+// runs after it (k_polish, one workgroup per series).
 #pragma once
 
 #define PF_TS 16   // series per tile (MFMA N)
 #define PF_TNW 4   // waves per tile workgroup
 #define PF_TH 5    // L-BFGS history (Stan default)
+#define PF_TV 64   // LDS stride of a per-series parameter vector
+#define PF_TNP 4   // parameters per lane (p = g + 16 i)
+#define PF_TSEG 33 // per-series stride of the segment tables (odd: conflict-free LDS reads)
 
 struct TileZ {
   double fk, fk1, fq, gpq, alpha, alphak_1, dfp, c1dfp, c2dfp, alpha0, alpha1, prevF, prevDFp;
@@ -41,11 +51,10 @@ template <int MODE>
 struct TileSmem {
   static constexpr int NSET = ((MODE & 3) == 2) ? 2 : 1;
   static constexpr int KP = 32;  // padded feature count (K <= 32)
-  int V;                         // per-series vector stride (doubles)
-  double *xk, *gk, *pk, *xq, *gq;  // [16][V]
-  double *hs, *hy;               // [H][16][V]
+  double *xk, *gk, *pk, *xq, *gq;  // [16][PF_TV]
+  double *hs, *hy;               // [H][16][PF_TV]
   double *hrho;                  // [16][H]
-  double *kseg, *mseg;           // [16][32]
+  double *kseg, *mseg;           // [16][PF_TSEG]
   double *bm, *ba;               // [KP][16]
   double *gb;                    // [NSET][KP][16]
   double *sg0, *sg1;             // [32][16] segment sums of G, G t
@@ -54,17 +63,16 @@ struct TileSmem {
   double *ctc, *csg, *csm, *csa; // [64]
   TileZ *z;                      // [16]
   int *flag;                     // [4]
-  static __host__ __device__ int vstride(int P) { return 4 * ((P + 3) / 4) + 4; }
-  static __host__ __device__ size_t bytes(int P) {
-    const size_t V = (size_t)vstride(P);
-    const size_t d = (5 + 2 * PF_TH) * PF_TS * V + PF_TS * PF_TH + 2 * PF_TS * 32 +
-                     2 * KP * PF_TS + NSET * KP * PF_TS + 2 * 32 * PF_TS + PF_TS + 2 * PF_TS + 4 * 64;
+  // gb, sg0, sg1, rr are contiguous: zeroed as one block per evaluation
+  static constexpr size_t acc_doubles() { return NSET * KP * PF_TS + 2 * 32 * PF_TS + PF_TS; }
+  static __host__ __device__ size_t bytes() {
+    const size_t d = (5 + 2 * PF_TH) * PF_TS * PF_TV + PF_TS * PF_TH + 2 * PF_TS * PF_TSEG +
+                     2 * KP * PF_TS + acc_doubles() + 2 * PF_TS + 4 * 64;
     return d * sizeof(double) + PF_TS * sizeof(TileZ) + 64;
   }
-  __device__ void carve(char *base, int P) {
-    V = vstride(P);
+  __device__ void carve(char *base) {
     double *p = reinterpret_cast<double *>(base);
-    const size_t vec = (size_t)PF_TS * V;
+    constexpr size_t vec = (size_t)PF_TS * PF_TV;
     xk = p; p += vec;
     gk = p; p += vec;
     pk = p; p += vec;
@@ -73,8 +81,8 @@ struct TileSmem {
     hs = p; p += PF_TH * vec;
     hy = p; p += PF_TH * vec;
     hrho = p; p += PF_TS * PF_TH;
-    kseg = p; p += PF_TS * 32;
-    mseg = p; p += PF_TS * 32;
+    kseg = p; p += PF_TS * PF_TSEG;
+    mseg = p; p += PF_TS * PF_TSEG;
     bm = p; p += KP * PF_TS;
     ba = p; p += KP * PF_TS;
     gb = p; p += NSET * KP * PF_TS;
@@ -91,132 +99,196 @@ struct TileSmem {
   }
 };
 
-// sum over the 4 lanes of a quad (uniform within the quad)
-__device__ __forceinline__ double quad_sum(double v) {
-  v += dpp_f64<PF_DPP_QXOR1>(v);
-  v += dpp_f64<PF_DPP_QXOR2>(v);
+// sum over the 16 lanes of a series group (bitwise uniform within the group:
+// each butterfly stage adds the same two partial sums in both lanes)
+__device__ __forceinline__ double grp_sum(double v) {
+  v += shfl_xor_f64<1>(v);
+  v += shfl_xor_f64<2>(v);
+  v += shfl_xor_f64<4>(v);
+  v += shfl_xor_f64<8>(v);
   return v;
 }
 
-// Publish series j's trial point xq: segment tables, beta o s_m / s_a, sigma.
-// Lane quad of series j; q = lane & 3.
+typedef double TVec[PF_TNP];
+
+__device__ __forceinline__ double tvdot(const TVec &u, const TVec &v) {
+  const double s = fma(u[0], v[0], u[1] * v[1]) + fma(u[2], v[2], u[3] * v[3]);
+  return grp_sum(s);
+}
+// LDS vector <-> registers; entries past P read as 0
+__device__ __forceinline__ void tvload(TVec &r, const double *v, int P, int g) {
+#pragma unroll
+  for (int i = 0; i < PF_TNP; ++i) {
+    const int p = g + 16 * i;
+    r[i] = (p < P) ? v[p] : 0.0;
+  }
+}
+__device__ __forceinline__ void tvstore(double *v, const TVec &r, int P, int g) {
+#pragma unroll
+  for (int i = 0; i < PF_TNP; ++i) {
+    const int p = g + 16 * i;
+    if (p < P) v[p] = r[i];
+  }
+}
+
+// Publish series j's trial point xq: segment tables, beta o s_m / s_a, sigma
+// (the 16 lanes of series j; g = lane & 15).
 template <int MODE>
-__device__ __forceinline__ void tile_publish(const FitKArgs &a, TileSmem<MODE> &sm, int j, int q) {
-  const int S = a.S, K = a.K, V = sm.V;
-  const double *x = sm.xq + (size_t)j * V;
-  if (q == 0) {
-    const double k = x[0], m = x[1];
+__device__ __forceinline__ void tile_publish(const FitKArgs &a, TileSmem<MODE> &sm, int j, int g) {
+  const int S = a.S, K = a.K;
+  const double *x = sm.xq + (size_t)j * PF_TV;
+  if (g == 0) {
+    // flat growth: k = 0 and no slope changes in the tables (trend = m)
+    const bool lin = a.growth == PF_GROWTH_LINEAR;
+    const double k = lin ? x[0] : 0.0, m = x[1];
     double cd = 0.0, ctd = 0.0;
-    sm.kseg[j * 32] = k;
-    sm.mseg[j * 32] = m;
+    sm.kseg[j * PF_TSEG] = k;
+    sm.mseg[j * PF_TSEG] = m;
     for (int jj = 0; jj < S; ++jj) {
-      const double d = x[2 + jj];
+      const double d = lin ? x[2 + jj] : 0.0;
       cd += d;
       ctd = fma(sm.ctc[jj], d, ctd);
-      sm.kseg[j * 32 + jj + 1] = k + cd;
-      sm.mseg[j * 32 + jj + 1] = m - ctd;
+      sm.kseg[j * PF_TSEG + jj + 1] = k + cd;
+      sm.mseg[j * PF_TSEG + jj + 1] = m - ctd;
     }
+  }
+  if (g == 1) {
     const double sg = exp(x[2 + S]);
     sm.sig[2 * j] = sg;
     sm.sig[2 * j + 1] = 1.0 / (sg * sg);
   }
-  for (int f = q; f < TileSmem<MODE>::KP; f += 4) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int f = g + 16 * h;
     const double bv = (f < K) ? x[3 + S + f] : 0.0;
     sm.bm[f * PF_TS + j] = bv * sm.csm[f];
     sm.ba[f * PF_TS + j] = bv * sm.csa[f];
   }
 }
 
-// Row pass of one evaluation (all waves): per 16-row chunk, Xb on MFMA,
-// elementwise residual / likelihood terms in the C layout, the beta
-// gradient on MFMA, segment sums of G and G t.  Accumulates into LDS
-// (gb, sg0/sg1, rr), which the caller zeroed.
-// one chunk's global inputs (loaded a chunk ahead: with one wave per SIMD
-// nothing else hides the L2 / HBM latency)
+typedef double pf_d2 __attribute__((ext_vector_type(2)));
+typedef int pf_i4 __attribute__((ext_vector_type(4)));
+
+// Row mapping inside a 16-row chunk: C-layout row i (lane (j, rq) register
+// rg holds C-row rq + 4 rg) is data row r0 + 4 (i & 3) + (i >> 2), so each
+// lane's four rows are contiguous (t, y, seg in two / one wide loads) and
+// k-step q of X'W covers data rows r0 + 4 rq + q.  Feature maps: Xb k-step
+// kk, lane k index rq <-> feature 8 rq + kk; X'W tile ft, output row i <->
+// feature 2 i + ft (both contiguous per lane in the row-major copy XR).
 struct TileIn {
-  double xa[8];      // Xb A operand, k-step kk: X[row r0 + (lane & 15)][4kk + (lane >> 4)]
-  double xg[2][4];   // X'W A operand: X[row r0 + (lane >> 4) + 4q][16 ft + (lane & 15)]
-  double t[4], y[4]; // C-layout rows r0 + (lane >> 4) + 4 rg
-  int sg[4];
-  int sfirst, slast;
+  pf_d2 xa[4];  // X[r0 + 4 (j & 3) + (j >> 2)][8 rq + 2h .. +1]  (Xb k-steps 2h, 2h+1)
+  pf_d2 xg[4];  // X[r0 + 4 rq + q][2 j .. 2 j + 1]             (X'W k-step q, tiles 0/1)
+  pf_d2 t[2], y[2];  // data rows r0 + 4 rq + rg
+  pf_i4 sg;
 };
 
+// Row pass of one evaluation (all waves): accumulates the beta gradient
+// tiles, segment sums of G / G t and the residual sum of squares into LDS
+// (gb, sg0/sg1, rr), which the caller zeroed.
 template <int MODE>
 __device__ __forceinline__ void tile_rows(const FitKArgs &a, TileSmem<MODE> &sm, int tile, int n) {
   constexpr int NSET = TileSmem<MODE>::NSET;
+  constexpr bool HM = (MODE & 3) != MODE_ADD, HA = (MODE & 3) != MODE_MULT;
   const int lane = pf_lane(), wave = pf_wave();
-  const int T = a.T, Tp = a.Tp, K = a.K;
+  const int T = a.T, Tp = a.Tp;
   const int j = lane & 15, rq = lane >> 4;
-  const bool linear = a.growth == PF_GROWTH_LINEAR;
   const int s_g = tile * PF_TS + j;
   const bool svalid = s_g < n;
   const double *ys = a.y_scaled + (size_t)(svalid ? s_g : 0) * Tp;
-  const double *XT = a.XT;
-  // B operands of Xb: k-step kk covers features 4kk..4kk+3 (lane: k = rq)
+  const double *XR = a.XR;
+  const double *kseg = sm.kseg + j * PF_TSEG, *mseg = sm.mseg + j * PF_TSEG;
+  const int jrow = 4 * (j & 3) + (j >> 2);
+  // B operands of Xb: k-step kk, lane k index rq <-> feature 8 rq + kk
   double bmr[8], bar_[8];
 #pragma unroll
   for (int kk = 0; kk < 8; ++kk) {
-    bmr[kk] = ((MODE & 3) != MODE_ADD) ? sm.bm[(4 * kk + rq) * PF_TS + j] : 0.0;
-    bar_[kk] = ((MODE & 3) != MODE_MULT) ? sm.ba[(4 * kk + rq) * PF_TS + j] : 0.0;
+    bmr[kk] = HM ? sm.bm[(8 * rq + kk) * PF_TS + j] : 0.0;
+    bar_[kk] = HA ? sm.ba[(8 * rq + kk) * PF_TS + j] : 0.0;
   }
-  const int nkk = (K + 3) >> 2;
+  // unconditional wide loads (T_pad % 128 == 0 keeps every chunk row in
+  // range; XR is zero past K): no predicated load to drain the prefetch
   auto tload = [&](int c, TileIn &in) {
     const int r0 = 16 * c;
+    const pf_d2 *xa = reinterpret_cast<const pf_d2 *>(XR + (size_t)(r0 + jrow) * 32 + 8 * rq);
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) {
-      const int f = 4 * kk + rq;
-      in.xa[kk] = (kk < nkk && f < K) ? XT[(size_t)f * Tp + r0 + j] : 0.0;
+    for (int h = 0; h < 4; ++h) in.xa[h] = xa[h];
+    const pf_d2 *xg = reinterpret_cast<const pf_d2 *>(XR + (size_t)(r0 + 4 * rq) * 32 + 2 * j);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) in.xg[q] = xg[q * 16];
+    const pf_d2 *tt = reinterpret_cast<const pf_d2 *>(a.t + r0 + 4 * rq);
+    const pf_d2 *yy = reinterpret_cast<const pf_d2 *>(ys + r0 + 4 * rq);
+    in.t[0] = tt[0];
+    in.t[1] = tt[1];
+    in.y[0] = yy[0];
+    in.y[1] = yy[1];
+    in.sg = *reinterpret_cast<const pf_i4 *>(a.seg + r0 + 4 * rq);
+  };
+  auto xb_mfma = [&](const TileIn &in, pf_d4 &xm, pf_d4 &xa) {
+    // two independent accumulation chains per product (even / odd k-steps)
+    pf_d4 m0 = pf_d4{0.0, 0.0, 0.0, 0.0}, m1 = m0, a0_ = m0, a1_ = m0;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      if constexpr (HM) {
+        m0 = __builtin_amdgcn_mfma_f64_16x16x4f64(in.xa[h][0], bmr[2 * h], m0, 0, 0, 0);
+        m1 = __builtin_amdgcn_mfma_f64_16x16x4f64(in.xa[h][1], bmr[2 * h + 1], m1, 0, 0, 0);
+      }
+      if constexpr (HA) {
+        a0_ = __builtin_amdgcn_mfma_f64_16x16x4f64(in.xa[h][0], bar_[2 * h], a0_, 0, 0, 0);
+        a1_ = __builtin_amdgcn_mfma_f64_16x16x4f64(in.xa[h][1], bar_[2 * h + 1], a1_, 0, 0, 0);
+      }
     }
-#pragma unroll
-    for (int ft = 0; ft < 2; ++ft) {
-      const int f = 16 * ft + j;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) in.xg[ft][q] = (f < K) ? XT[(size_t)f * Tp + r0 + rq + 4 * q] : 0.0;
-    }
-#pragma unroll
-    for (int rg = 0; rg < 4; ++rg) {
-      const int row = r0 + rq + 4 * rg;
-      in.t[rg] = a.t[row];
-      in.sg[rg] = a.seg[row];
-      in.y[rg] = (svalid && row < T) ? ys[row] : 0.0;
-    }
-    in.sfirst = a.seg[r0];
-    in.slast = a.seg[min(r0 + 15, T - 1)];
+    xm = m0 + m1;
+    xa = a0_ + a1_;
   };
   pf_d4 gbm[2], gba[2];
 #pragma unroll
-  for (int ft = 0; ft < 2; ++ft) { gbm[ft] = pf_d4{0.0, 0.0, 0.0, 0.0}; gba[ft] = pf_d4{0.0, 0.0, 0.0, 0.0}; }
+  for (int ft = 0; ft < 2; ++ft) { gbm[ft] = pf_d4{0.0, 0.0, 0.0, 0.0}; gba[ft] = gbm[ft]; }
   double rr = 0.0, a0 = 0.0, a1 = 0.0;
   int cur = -1;
+  auto flush = [&]() {
+    double b0 = a0 + shfl_xor_f64<16>(a0), b1 = a1 + shfl_xor_f64<16>(a1);
+    b0 += shfl_xor_f64<32>(b0);
+    b1 += shfl_xor_f64<32>(b1);
+    if (rq == 0) {
+      atomicAdd(&sm.sg0[cur * PF_TS + j], b0);
+      atomicAdd(&sm.sg1[cur * PF_TS + j], b1);
+    }
+  };
   const int nch = (T + 15) >> 4;
   const int c0 = (nch * wave) / PF_TNW, c1 = (nch * (wave + 1)) / PF_TNW;
-  TileIn nx;
-  if (c0 < c1) tload(c0, nx);
-  for (int c = c0; c < c1; ++c) {
-    const TileIn cu = nx;
-    if (c + 1 < c1) tload(c + 1, nx);
+  // one chunk: loads of chunk c + 2 into `nn`, Xb of chunk c + 1 (`nx`) on
+  // the matrix pipe, then chunk c's (`cu`, Xb in `xc`) elementwise work and
+  // X'W.  Input and Xb buffers rotate three ways: no register copies of
+  // in-flight loads or MFMA results.
+  auto step = [&](int c, const TileIn &cu, const TileIn &nx, TileIn &nn, const pf_d4 &xcm,
+                  const pf_d4 &xca, pf_d4 &xnm, pf_d4 &xna) {
     const int r0 = 16 * c;
-    // Xb = X[16 rows x K] . B[K x 16]
-    pf_d4 xbm = pf_d4{0.0, 0.0, 0.0, 0.0}, xba = pf_d4{0.0, 0.0, 0.0, 0.0};
+    const int rbase = r0 + 4 * rq;
+    // trend k_s t + m_s from the per-series segment tables (flat growth:
+    // k = 0, one m); reads issued before the Xb MFMAs of the next chunk
+    double ks[4], ms[4];
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) {
-      if (kk < nkk) {
-        if constexpr ((MODE & 3) != MODE_ADD) xbm = __builtin_amdgcn_mfma_f64_16x16x4f64(cu.xa[kk], bmr[kk], xbm, 0, 0, 0);
-        if constexpr ((MODE & 3) != MODE_MULT) xba = __builtin_amdgcn_mfma_f64_16x16x4f64(cu.xa[kk], bar_[kk], xba, 0, 0, 0);
-      }
+    for (int rg = 0; rg < 4; ++rg) {
+      ks[rg] = kseg[cu.sg[rg]];
+      ms[rg] = mseg[cu.sg[rg]];
     }
-    // elementwise on the C layout: element rg is (row r0 + rq + 4 rg, series j)
+    tload(min(c + 2, c1 - 1), nn);
+    xb_mfma(nx, xnm, xna);
+    // chunk-uniform segment (all valid rows in one segment): register sums
+    const int s0 = __builtin_amdgcn_readfirstlane(cu.sg[0]);
+    const bool same = (cu.sg[0] == s0 || rbase >= T) && (cu.sg[1] == s0 || rbase + 1 >= T) &&
+                      (cu.sg[2] == s0 || rbase + 2 >= T) && (cu.sg[3] == s0 || rbase + 3 >= T);
+    const bool uni = __ballot(!same) == 0ull;
     double W[4], Wa[4], G[4], Gt[4];
 #pragma unroll
     for (int rg = 0; rg < 4; ++rg) {
-      const int row = r0 + rq + 4 * rg;
+      const int row = rbase + rg;
       const bool v = svalid && row < T;
-      const double ti = cu.t[rg];
-      const int sg = cu.sg[rg];
-      const double tr = linear ? fma(sm.kseg[j * 32 + sg], ti, sm.mseg[j * 32 + sg]) : sm.mseg[j * 32];
-      const double u = 1.0 + (((MODE & 3) != MODE_ADD) ? xbm[rg] : 0.0);
-      const double mu = fma(tr, u, ((MODE & 3) != MODE_MULT) ? xba[rg] : 0.0);
-      const double r = v ? cu.y[rg] - mu : 0.0;
+      const double ti = cu.t[rg >> 1][rg & 1];
+      const double tr = fma(ks[rg], ti, ms[rg]);
+      const double u = 1.0 + (HM ? xcm[rg] : 0.0);
+      const double mu = fma(tr, u, HA ? xca[rg] : 0.0);
+      const double r = v ? cu.y[rg >> 1][rg & 1] - mu : 0.0;
       rr = fma(r, r, rr);
       W[rg] = r * tr;
       Wa[rg] = r;
@@ -228,110 +300,101 @@ __device__ __forceinline__ void tile_rows(const FitKArgs &a, TileSmem<MODE> &sm,
     for (int q = 0; q < 4; ++q) {
 #pragma unroll
       for (int ft = 0; ft < 2; ++ft) {
-        if constexpr ((MODE & 3) != MODE_ADD) gbm[ft] = __builtin_amdgcn_mfma_f64_16x16x4f64(cu.xg[ft][q], W[q], gbm[ft], 0, 0, 0);
-        if constexpr ((MODE & 3) != MODE_MULT) gba[ft] = __builtin_amdgcn_mfma_f64_16x16x4f64(cu.xg[ft][q], Wa[q], gba[ft], 0, 0, 0);
+        if constexpr (HM) gbm[ft] = __builtin_amdgcn_mfma_f64_16x16x4f64(cu.xg[q][ft], W[q], gbm[ft], 0, 0, 0);
+        if constexpr (HA) gba[ft] = __builtin_amdgcn_mfma_f64_16x16x4f64(cu.xg[q][ft], Wa[q], gba[ft], 0, 0, 0);
       }
     }
     // changepoint adjoint: segment sums of G, G t per series
-    if (cu.sfirst == cu.slast) {
-      const double g0 = (G[0] + G[1]) + (G[2] + G[3]), g1 = (Gt[0] + Gt[1]) + (Gt[2] + Gt[3]);
-      if (cu.sfirst != cur) {
-        if (cur >= 0) {
-          double b0 = a0 + shfl_xor_f64<16>(a0), b1 = a1 + shfl_xor_f64<16>(a1);
-          b0 += shfl_xor_f64<32>(b0);
-          b1 += shfl_xor_f64<32>(b1);
-          if (rq == 0) {
-            atomicAdd(&sm.sg0[cur * PF_TS + j], b0);
-            atomicAdd(&sm.sg1[cur * PF_TS + j], b1);
-          }
-        }
-        cur = cu.sfirst;
+    if (uni) {
+      if (s0 != cur) {
+        if (cur >= 0) flush();
+        cur = s0;
         a0 = 0.0;
         a1 = 0.0;
       }
-      a0 += g0;
-      a1 += g1;
+      a0 += (G[0] + G[1]) + (G[2] + G[3]);
+      a1 += (Gt[0] + Gt[1]) + (Gt[2] + Gt[3]);
     } else {
 #pragma unroll
       for (int rg = 0; rg < 4; ++rg) {
-        const int row = r0 + rq + 4 * rg;
-        if (row < T) {
+        if (rbase + rg < T) {
           atomicAdd(&sm.sg0[cu.sg[rg] * PF_TS + j], G[rg]);
           atomicAdd(&sm.sg1[cu.sg[rg] * PF_TS + j], Gt[rg]);
         }
       }
     }
-  }
-  if (cur >= 0) {
-    double b0 = a0 + shfl_xor_f64<16>(a0), b1 = a1 + shfl_xor_f64<16>(a1);
-    b0 += shfl_xor_f64<32>(b0);
-    b1 += shfl_xor_f64<32>(b1);
-    if (rq == 0) {
-      atomicAdd(&sm.sg0[cur * PF_TS + j], b0);
-      atomicAdd(&sm.sg1[cur * PF_TS + j], b1);
+  };
+  if (c0 < c1) {
+    TileIn A, B, C;
+    pf_d4 XAm, XAa, XBm, XBa, XCm, XCa;
+    tload(c0, A);
+    tload(min(c0 + 1, c1 - 1), B);
+    xb_mfma(A, XAm, XAa);
+    for (int c = c0; c < c1; c += 3) {
+      step(c, A, B, C, XAm, XAa, XBm, XBa);
+      if (c + 1 < c1) step(c + 1, B, C, A, XBm, XBa, XCm, XCa);
+      if (c + 2 < c1) step(c + 2, C, A, B, XCm, XCa, XAm, XAa);
     }
   }
+  if (cur >= 0) flush();
   rr += shfl_xor_f64<16>(rr);
   rr += shfl_xor_f64<32>(rr);
   if (rq == 0) atomicAdd(&sm.rr[j], rr);
-  // gradient tiles: C[feature 16 ft + rq + 4 rg][series j]
+  // gradient tiles: C[row i = rq + 4 rg][series j] of tile ft is feature 2 i + ft
 #pragma unroll
   for (int ft = 0; ft < 2; ++ft)
 #pragma unroll
     for (int rg = 0; rg < 4; ++rg) {
-      const int f = 16 * ft + rq + 4 * rg;
-      if constexpr ((MODE & 3) != MODE_ADD) atomicAdd(&sm.gb[f * PF_TS + j], gbm[ft][rg]);
-      if constexpr ((MODE & 3) != MODE_MULT)
-        atomicAdd(&sm.gb[(NSET - 1) * TileSmem<MODE>::KP * PF_TS + f * PF_TS + j], gba[ft][rg]);
+      const int f = 2 * (rq + 4 * rg) + ft;
+      if constexpr (HM) atomicAdd(&sm.gb[f * PF_TS + j], gbm[ft][rg]);
+      if constexpr (HA) atomicAdd(&sm.gb[(NSET - 1) * TileSmem<MODE>::KP * PF_TS + f * PF_TS + j], gba[ft][rg]);
     }
 }
 
-// wave 0, lane quad of series j: f and g at xq (this lane's parameters
-// p = q + 4i -> gq), gpq = g . pk.  Returns true if not finite.
+// f and g of series j at xq (lane g: parameters g + 16 i -> sm.gq), gpq =
+// g . pk.  Returns true if not finite (group-uniform).
 template <int MODE>
-__device__ __forceinline__ bool tile_assemble(const FitKArgs &a, TileSmem<MODE> &sm, int j, int q,
+__device__ __forceinline__ bool tile_assemble(const FitKArgs &a, TileSmem<MODE> &sm, int j, int g,
                                               double &f, double &gpq) {
   constexpr int NSET = TileSmem<MODE>::NSET;
-  const int S = a.S, K = a.K, P = a.P, T = a.T, V = sm.V;
+  const int S = a.S, P = a.P, T = a.T;
   const bool linear = a.growth == PF_GROWTH_LINEAR;
-  const double *x = sm.xq + (size_t)j * V;
-  double *g = sm.gq + (size_t)j * V;
-  const double *pk = sm.pk + (size_t)j * V;
+  const double *x = sm.xq + (size_t)j * PF_TV;
+  double *gv_out = sm.gq + (size_t)j * PF_TV;
+  const double *pk = sm.pk + (size_t)j * PF_TV;
   const double sigma = sm.sig[2 * j], inv = sm.sig[2 * j + 1], tau = a.tau;
   const double rrt = sm.rr[j];
-  // totals and suffix sums over segments (redundant in the quad's lanes)
-  double tot0 = 0.0, tot1 = 0.0;
-  for (int s = 0; s <= S; ++s) { tot0 += sm.sg0[s * PF_TS + j]; tot1 += sm.sg1[s * PF_TS + j]; }
+  // segment totals: lane g holds segments g and g + 16 (S + 1 <= 32)
+  const double s0a = (g <= S) ? sm.sg0[g * PF_TS + j] : 0.0;
+  const double s1a = (g <= S) ? sm.sg1[g * PF_TS + j] : 0.0;
+  const double s0b = (g + 16 <= S) ? sm.sg0[(g + 16) * PF_TS + j] : 0.0;
+  const double s1b = (g + 16 <= S) ? sm.sg1[(g + 16) * PF_TS + j] : 0.0;
+  const double tot0 = grp_sum(s0a + s0b), tot1 = grp_sum(s1a + s1b);
   double fl = 0.0, gp = 0.0;
   bool bad = false;
-  // delta_jj: sum over segments s > jj of (G t - tc_jj G)
-  {
-    double su0 = 0.0, su1 = 0.0;
-    for (int s = S; s >= 1; --s) {
-      su0 += sm.sg0[s * PF_TS + j];
-      su1 += sm.sg1[s * PF_TS + j];
-      const int p = 2 + (s - 1);
-      if ((p & 3) == q) {
-        const double d = x[p];
-        const double sgn = (d > 0.0) - (d < 0.0);
-        const double gv = (linear ? -inv * (su1 - sm.ctc[s - 1] * su0) : 0.0) + sgn / tau;
-        g[p] = gv;
-        fl += fabs(d) / tau;
-        gp = fma(gv, pk[p], gp);
-        bad |= !isfinite(gv);
-      }
-    }
-  }
-  for (int p = q; p < P; p += 4) {
-    if (p >= 2 && p < 2 + S) continue;
-    double gv, ft;
+#pragma unroll
+  for (int i = 0; i < PF_TNP; ++i) {
+    const int p = g + 16 * i;
+    if (p >= P) continue;
     const double xv = x[p];
+    double gv, ft;
     if (p == 0) {
       gv = -inv * (linear ? tot1 : 0.0) + xv / 25.0;
       ft = xv * xv / 50.0;
     } else if (p == 1) {
       gv = -inv * tot0 + xv / 25.0;
       ft = xv * xv / 50.0;
+    } else if (p < 2 + S) {
+      // changepoint jj is active in segments s > jj
+      const int jj = p - 2;
+      double su0 = 0.0, su1 = 0.0;
+      for (int s = jj + 1; s <= S; ++s) {
+        su0 += sm.sg0[s * PF_TS + j];
+        su1 += sm.sg1[s * PF_TS + j];
+      }
+      const double sgn = (xv > 0.0) - (xv < 0.0);
+      gv = (linear ? -inv * (su1 - sm.ctc[jj] * su0) : 0.0) + sgn / tau;
+      ft = fabs(xv) / tau;
     } else if (p == 2 + S) {
       gv = (double)T - inv * rrt + 4.0 * sigma * sigma;
       ft = 2.0 * sigma * sigma + (double)T * xv;
@@ -345,69 +408,37 @@ __device__ __forceinline__ bool tile_assemble(const FitKArgs &a, TileSmem<MODE> 
       gv = -inv * gl + xv / (sgm * sgm);
       ft = xv * xv / (2.0 * sgm * sgm);
     }
-    g[p] = gv;
+    gv_out[p] = gv;
     fl += ft;
     gp = fma(gv, pk[p], gp);
     bad |= !isfinite(gv);
   }
-  f = quad_sum(fl) + 0.5 * rrt * inv;
-  gpq = quad_sum(gp);
+  f = grp_sum(fl) + 0.5 * rrt * inv;
+  gpq = grp_sum(gp);
   bad |= !isfinite(f);
-  // quad-uniform
-  const int b = bad ? 1 : 0;
-  return (b | __shfl_xor(b, 1, 64) | __shfl_xor(b, 2, 64)) != 0;
-}
-
-#define PF_TNP 15  // parameters per lane (p = q + 4i, P <= 60)
-typedef double TVec[PF_TNP];
-
-__device__ __forceinline__ double tvdot(const TVec &u, const TVec &v) {
-  double s0 = 0.0, s1 = 0.0;
-#pragma unroll
-  for (int i = 0; i < PF_TNP; i += 2) {
-    s0 = fma(u[i], v[i], s0);
-    if (i + 1 < PF_TNP) s1 = fma(u[i + 1], v[i + 1], s1);
-  }
-  return quad_sum(s0 + s1);
-}
-// LDS vector (series stride V) <-> registers; entries past P read as 0
-__device__ __forceinline__ void tvload(TVec &r, const double *v, int P, int q) {
-#pragma unroll
-  for (int i = 0; i < PF_TNP; ++i) {
-    const int p = q + 4 * i;
-    r[i] = (p < P) ? v[p] : 0.0;
-  }
-}
-__device__ __forceinline__ void tvstore(double *v, const TVec &r, int P, int q) {
-#pragma unroll
-  for (int i = 0; i < PF_TNP; ++i) {
-    const int p = q + 4 * i;
-    if (p < P) v[p] = r[i];
-  }
+  return grp_sum(bad ? 1.0 : 0.0) != 0.0;
 }
 
 // Stan 2.19 BFGSMinimizer<LBFGSUpdate>::step + WolfeLineSearch as a per-series
-// state machine (lane quad): advance until the series needs an evaluation
-// at xq (returns true) or terminates (false, z.ret set).  Same control flow
-// as lbfgs_step (pf_engine.hip) and oracle/stan_lbfgs.c; the search direction
+// state machine (16 lanes): advance until the series needs an evaluation at
+// xq (returns true) or terminates (false, z.ret set).  Same control flow as
+// lbfgs_step (pf_engine.hip) and oracle/stan_lbfgs.c; the search direction
 // by Stan's two-loop recursion.  The working vectors live in registers for
-// the step (one batched LDS read per history vector).
+// the step (4 entries per lane).
 template <int MODE>
 __device__ __forceinline__ bool tile_lbfgs(const pf_fit_opts &o, TileSmem<MODE> &sm, TileZ &z, int j,
-                                           int q, int P) {
-  const int V = sm.V;
-  double *xkL = sm.xk + (size_t)j * V, *gkL = sm.gk + (size_t)j * V, *pkL = sm.pk + (size_t)j * V;
-  double *xqL = sm.xq + (size_t)j * V;
+                                           int g, int P) {
+  double *xkL = sm.xk + (size_t)j * PF_TV, *gkL = sm.gk + (size_t)j * PF_TV, *pkL = sm.pk + (size_t)j * PF_TV;
+  double *xqL = sm.xq + (size_t)j * PF_TV;
   const int H = o.history < PF_TH ? o.history : PF_TH;
-  const size_t hstep = (size_t)PF_TS * V;
+  constexpr size_t hstep = (size_t)PF_TS * PF_TV;
   TVec xk, gk, pk, xq, gq;
-  tvload(xk, xkL, P, q);
-  tvload(gk, gkL, P, q);
-  tvload(pk, pkL, P, q);
-  tvload(xq, xqL, P, q);
-  tvload(gq, sm.gq + (size_t)j * V, P, q);
-  bool need = false;
-  bool run = true;
+  tvload(xk, xkL, P, g);
+  tvload(gk, gkL, P, g);
+  tvload(pk, pkL, P, g);
+  tvload(xq, xqL, P, g);
+  tvload(gq, sm.gq + (size_t)j * PF_TV, P, g);
+  bool need = false, run = true;
   while (run) {
     switch (z.state) {
       case LB_INIT:
@@ -566,12 +597,14 @@ __device__ __forceinline__ bool tile_lbfgs(const pf_fit_opts &o, TileSmem<MODE> 
         } else {
           // LBFGSUpdate::update (store the pair) + search_direction (two loops)
           z.gammak = sy / yy;
-          tvstore(sm.hs + slot * hstep + (size_t)j * V, sk, P, q);
-          tvstore(sm.hy + slot * hstep + (size_t)j * V, yk, P, q);
-          if (q == 0) sm.hrho[j * PF_TH + slot] = 1.0 / sy;
+          const double rho_new = 1.0 / sy;
+          tvstore(sm.hs + slot * hstep + (size_t)j * PF_TV, sk, P, g);
+          tvstore(sm.hy + slot * hstep + (size_t)j * PF_TV, yk, P, g);
+          if (g == 0) sm.hrho[j * PF_TH + slot] = rho_new;
           if (z.hcount < H) z.hcount++;
           else z.head = pf_wrap(z.head + 1, H);
           __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+          __builtin_amdgcn_wave_barrier();
 #pragma unroll
           for (int i = 0; i < PF_TNP; ++i) pk[i] = -gk[i];
           double al[PF_TH];
@@ -581,14 +614,17 @@ __device__ __forceinline__ bool tile_lbfgs(const pf_fit_opts &o, TileSmem<MODE> 
             if (c < z.hcount) {
               const int sl = pf_wrap(z.head + c, H);
               TVec sv, yv;
+              double rho_c;
               if (c == z.hcount - 1) {    // newest pair: still in registers
 #pragma unroll
                 for (int i = 0; i < PF_TNP; ++i) { sv[i] = sk[i]; yv[i] = yk[i]; }
+                rho_c = rho_new;
               } else {
-                tvload(sv, sm.hs + sl * hstep + (size_t)j * V, P, q);
-                tvload(yv, sm.hy + sl * hstep + (size_t)j * V, P, q);
+                tvload(sv, sm.hs + sl * hstep + (size_t)j * PF_TV, P, g);
+                tvload(yv, sm.hy + sl * hstep + (size_t)j * PF_TV, P, g);
+                rho_c = sm.hrho[j * PF_TH + sl];
               }
-              al[c] = sm.hrho[j * PF_TH + sl] * tvdot(sv, pk);
+              al[c] = rho_c * tvdot(sv, pk);
 #pragma unroll
               for (int i = 0; i < PF_TNP; ++i) pk[i] = fma(-al[c], yv[i], pk[i]);
             }
@@ -600,9 +636,17 @@ __device__ __forceinline__ bool tile_lbfgs(const pf_fit_opts &o, TileSmem<MODE> 
             if (c < z.hcount) {
               const int sl = pf_wrap(z.head + c, H);
               TVec sv, yv;
-              tvload(sv, sm.hs + sl * hstep + (size_t)j * V, P, q);
-              tvload(yv, sm.hy + sl * hstep + (size_t)j * V, P, q);
-              const double b = sm.hrho[j * PF_TH + sl] * tvdot(yv, pk);
+              double rho_c;
+              if (c == z.hcount - 1) {
+#pragma unroll
+                for (int i = 0; i < PF_TNP; ++i) { sv[i] = sk[i]; yv[i] = yk[i]; }
+                rho_c = rho_new;
+              } else {
+                tvload(sv, sm.hs + sl * hstep + (size_t)j * PF_TV, P, g);
+                tvload(yv, sm.hy + sl * hstep + (size_t)j * PF_TV, P, g);
+                rho_c = sm.hrho[j * PF_TH + sl];
+              }
+              const double b = rho_c * tvdot(yv, pk);
 #pragma unroll
               for (int i = 0; i < PF_TNP; ++i) pk[i] = fma(al[c] - b, sv[i], pk[i]);
             }
@@ -622,28 +666,30 @@ __device__ __forceinline__ bool tile_lbfgs(const pf_fit_opts &o, TileSmem<MODE> 
         break;
     }
   }
-  tvstore(xkL, xk, P, q);
-  tvstore(gkL, gk, P, q);
-  tvstore(pkL, pk, P, q);
-  tvstore(xqL, xq, P, q);
+  tvstore(xkL, xk, P, g);
+  tvstore(gkL, gk, P, g);
+  tvstore(pkL, pk, P, g);
+  tvstore(xqL, xq, P, g);
   return need;
 }
 
 // K3T kernel: grid = ceil(n / 16) tiles.  Pass-0 semantics of fit_body
 // (theta in: init; out: the L-BFGS endpoint, f, f_stan, status, n_iter,
-// n_eval), warm = the iteration cap is the warm-up cap (MAXIT -> WARMUP).
+// n_eval); warm = the iteration cap is the warm-up cap (MAXIT -> WARMUP).
+// Per evaluation: row pass (all waves) | barrier | assemble (16 lanes per
+// series) | barrier | zero accumulators + L-BFGS step + publish | barrier.
 template <int MODE>
 __global__ __launch_bounds__(PF_TNW * 64, 1) void k_fit_tile(FitKArgs a, int n) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   TileSmem<MODE> sm;
-  sm.carve(smem_raw, a.P);
+  sm.carve(smem_raw);
   const int tile = blockIdx.x, lane = pf_lane(), wave = pf_wave();
-  const int P = a.P, S = a.S, V = sm.V;
-  const int j = lane >> 2, q = lane & 3;  // wave 0: lane quad of series j
+  const int P = a.P, S = a.S;
+  const int j = 4 * wave + (lane >> 4), g = lane & 15;  // series j's 16 lanes
   const int sgl = tile * PF_TS + j;
   const bool warm = a.warm_cap != 0;
   const pf_fit_opts o = a.o;
-  // constants
+  constexpr int NACC = (int)TileSmem<MODE>::acc_doubles();
   if (threadIdx.x < 64) {
     const int i = threadIdx.x;
     sm.ctc[i] = (i < S) ? a.t_change[i] : 0.0;
@@ -651,28 +697,24 @@ __global__ __launch_bounds__(PF_TNW * 64, 1) void k_fit_tile(FitKArgs a, int n) 
     sm.csm[i] = (i < a.K) ? a.s_m[i] : 0.0;
     sm.csa[i] = (i < a.K) ? a.s_a[i] : 0.0;
   }
-  __syncthreads();
-  if (wave == 0) {
+  for (int e = threadIdx.x; e < NACC; e += PF_TNW * 64) sm.gb[e] = 0.0;
+  {
     TileZ &z = sm.z[j];
     const bool live = sgl < n && a.status[sgl] != PF_ST_CONSTANT;
-    double *xq = sm.xq + (size_t)j * V, *xk = sm.xk + (size_t)j * V;
-    for (int p = q; p < V; p += 4) {
+    double *xq = sm.xq + (size_t)j * PF_TV, *xk = sm.xk + (size_t)j * PF_TV;
+    for (int p = g; p < PF_TV; p += 16) {
       const double v = (sgl < n && p < P) ? a.theta[(size_t)sgl * P + p] : 0.0;
       xq[p] = v;
       xk[p] = v;
     }
-    if (q == 0) {
+    if (g == 0) {
       memset(&z, 0, sizeof(TileZ));
       z.state = LB_INIT;
       z.done = live ? 0 : 1;
     }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    tile_publish<MODE>(a, sm, j, q);
   }
-  for (int e = threadIdx.x; e < TileSmem<MODE>::NSET * TileSmem<MODE>::KP * PF_TS; e += PF_TNW * 64) sm.gb[e] = 0.0;
-  for (int e = threadIdx.x; e < 32 * PF_TS; e += PF_TNW * 64) { sm.sg0[e] = 0.0; sm.sg1[e] = 0.0; }
-  if (threadIdx.x < PF_TS) sm.rr[threadIdx.x] = 0.0;
+  __syncthreads();
+  tile_publish<MODE>(a, sm, j, g);
   __syncthreads();
   while (true) {
     PF_STAMP(0);
@@ -681,49 +723,42 @@ __global__ __launch_bounds__(PF_TNW * 64, 1) void k_fit_tile(FitKArgs a, int n) 
     __syncthreads();
     PF_STAMP(2);
     PF_COUNT(7);
-    if (wave == 0) {
-      TileZ &z = sm.z[j];
-      double fq, gpq;
-      const bool bad = tile_assemble<MODE>(a, sm, j, q, fq, gpq);
-      PF_STAMP(3);
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      bool need = false;
-      if (!z.done) {
-        TileZ zl = z;          // quad-local copy; lane q == 0 writes it back
-        zl.fq = fq;
-        zl.gpq = gpq;
-        zl.bad = bad ? 1 : 0;
-        zl.n_eval++;
-        need = tile_lbfgs<MODE>(o, sm, zl, j, q, P);
-        if (!need) zl.done = 1;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        if (q == 0) z = zl;
-      }
-      PF_STAMP(4);
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      if (need) tile_publish<MODE>(a, sm, j, q);
-      const unsigned long long any = __ballot(need);
-      if (lane == 0) sm.flag[0] = any != 0ull ? 1 : 0;
-      // zero the accumulators for the next evaluation (wave 0 has read them)
-      for (int e = lane; e < TileSmem<MODE>::NSET * TileSmem<MODE>::KP * PF_TS; e += 64) sm.gb[e] = 0.0;
-      for (int e = lane; e < 32 * PF_TS; e += 64) { sm.sg0[e] = 0.0; sm.sg1[e] = 0.0; }
-      if (lane < PF_TS) sm.rr[lane] = 0.0;
-      PF_STAMP(5);
+    TileZ &z = sm.z[j];
+    double fq, gpq;
+    const bool bad = tile_assemble<MODE>(a, sm, j, g, fq, gpq);
+    PF_STAMP(3);
+    __syncthreads();       // every wave has read the accumulators
+    for (int e = threadIdx.x; e < NACC; e += PF_TNW * 64) sm.gb[e] = 0.0;
+    bool need = false;
+    TileZ zl = z;          // group-local copy; lane g == 0 writes it back
+    if (!zl.done) {
+      zl.fq = fq;
+      zl.gpq = gpq;
+      zl.bad = bad ? 1 : 0;
+      zl.n_eval++;
+      need = tile_lbfgs<MODE>(o, sm, zl, j, g, P);
+      if (!need) zl.done = 1;
     }
+    PF_STAMP(4);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (g == 0) z = zl;
+    if (need) tile_publish<MODE>(a, sm, j, g);
+    const unsigned long long any = __ballot(need);
+    if (lane == 0) sm.flag[wave] = any != 0ull ? 1 : 0;
+    PF_STAMP(5);
     __syncthreads();
     PF_STAMP(6);
-    if (!__builtin_amdgcn_readfirstlane(sm.flag[0])) break;
+    const int more = sm.flag[0] | sm.flag[1] | sm.flag[2] | sm.flag[3];
+    if (!__builtin_amdgcn_readfirstlane(more)) break;
   }
   // outputs (pass-0 semantics of fit_body)
-  if (wave == 0 && sgl < n) {
-    TileZ &z = sm.z[j];
+  if (sgl < n) {
+    const TileZ &z = sm.z[j];
     double *th = a.theta + (size_t)sgl * P;
     const int st_in = a.status[sgl];
     if (st_in == PF_ST_CONSTANT) {
-      if (q == 0) {
+      if (g == 0) {
         th[2 + S] = log(1e-9);
         a.f_out[sgl] = NAN;
         a.f_stan[sgl] = NAN;
@@ -731,9 +766,9 @@ __global__ __launch_bounds__(PF_TNW * 64, 1) void k_fit_tile(FitKArgs a, int n) 
         a.n_eval[sgl] = 0;
       }
     } else {
-      const double *xk = sm.xk + (size_t)j * V;
-      for (int p = q; p < P; p += 4) th[p] = xk[p];
-      if (q == 0) {
+      const double *xk = sm.xk + (size_t)j * PF_TV;
+      for (int p = g; p < P; p += 16) th[p] = xk[p];
+      if (g == 0) {
         int st = z.ret;
         if (warm && st == PF_ST_MAXIT) st = PF_ST_WARMUP;
         a.f_out[sgl] = z.fk;

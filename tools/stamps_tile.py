@@ -29,7 +29,7 @@ lib.pf_debug_stamps(buf, 1)
 v = np.array(list(buf), dtype=np.float64)
 ne = max(v[7], 1)
 ph = {"row pass (wave 0)": v[1] - v[0], "barrier wait": v[2] - v[1], "assemble": v[3] - v[2],
-      "lbfgs step": v[4] - v[3], "publish+zero": v[5] - v[4], "end barrier": v[6] - v[5]}
+      "barrier+zero+lbfgs": v[4] - v[3], "publish": v[5] - v[4], "end barrier": v[6] - v[5]}
 print(f"n={n} fit(polish=False) {dt*1e3:.1f} ms; tile 0: {ne:.0f} evaluations; "
       f"series0 n_eval={fit.n_eval[0].item()}")
 tot = sum(ph.values())

@@ -92,19 +92,40 @@ __global__ void k_lat(double *out, unsigned long long *cyc, const double *in) {
   t0 = tick(x);
   for (int i = 0; i < N; ++i) __syncthreads();
   t1 = tick(x); if (lane == 0) cyc[12] = t1 - t0;
+  // 13: f64 MFMA 16x16x4, dependent (same accumulator) and 4 independent chains
+  {
+    typedef double d4 __attribute__((ext_vector_type(4)));
+    d4 acc = d4{x, y, x, y}, a1 = acc, a2 = acc, a3 = acc;
+    t0 = tick(x);
+    for (int i = 0; i < N; ++i) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, acc, 0, 0, 0);
+    double s = acc[0] + acc[3];
+    t1 = tick(s); if (lane == 0) cyc[16] = t1 - t0;
+    x += s * 1e-30;
+    t0 = tick(x);
+    for (int i = 0; i < N; ++i) {
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, acc, 0, 0, 0);
+      a1 = __builtin_amdgcn_mfma_f64_16x16x4f64(y, x, a1, 0, 0, 0);
+      a2 = __builtin_amdgcn_mfma_f64_16x16x4f64(x, x, a2, 0, 0, 0);
+      a3 = __builtin_amdgcn_mfma_f64_16x16x4f64(y, y, a3, 0, 0, 0);
+    }
+    s = acc[0] + a1[1] + a2[2] + a3[3];
+    t1 = tick(s); if (lane == 0) cyc[17] = t1 - t0;
+    x += s * 1e-30;
+  }
   out[lane] = x;
 }
 int main() {
   double *out, *in; unsigned long long *cyc;
-  hipMalloc(&out, 64 * 8); hipMalloc(&in, 128 * 8); hipMalloc(&cyc, 16 * 8);
+  hipMalloc(&out, 64 * 8); hipMalloc(&in, 128 * 8); hipMalloc(&cyc, 18 * 8);
   double h[128]; for (int i = 0; i < 128; ++i) h[i] = 1.0 + i * 1e-3;
   hipMemcpy(in, h, sizeof h, hipMemcpyHostToDevice);
   for (int rep = 0; rep < 2; ++rep) hipLaunchKernelGGL(k_lat, dim3(1), dim3(64), 0, 0, out, cyc, in);
-  unsigned long long c[16]; (void)hipMemcpy(c, cyc, sizeof(c[0]) * 16, hipMemcpyDeviceToHost);
+  unsigned long long c[18]; (void)hipMemcpy(c, cyc, sizeof(c[0]) * 18, hipMemcpyDeviceToHost);
   const char *nm[] = {"fma_f64 dep", "wave_sum f64", "lds read dep", "div f64", "readlane f64 -> valu",
                       "dpp row_shr f64 step", "permlane32 f64 step", "ds_bpermute f64", "fma_f64 8 indep chains (per iter)",
                       "wave_sum_multi<22>", "exp f64", "sqrt f64", "s_barrier (1 wave)",
-                      "xor16 (permlane16_swap) f64 step", "xor8 (dpp ror) f64 step", "xor4 (dpp shl/shr+sel) f64 step"};
-  for (int i = 0; i < 16; ++i) printf("%-34s %8.1f cycles/op\n", nm[i], (double)c[i] / N);
+                      "xor16 (permlane16_swap) f64 step", "xor8 (dpp ror) f64 step", "xor4 (dpp shl/shr+sel) f64 step",
+                      "mfma f64 16x16x4 dependent", "mfma f64 16x16x4 x4 indep (per iter)"};
+  for (int i = 0; i < 18; ++i) printf("%-34s %8.1f cycles/op\n", nm[i], (double)c[i] / N);
   return 0;
 }
