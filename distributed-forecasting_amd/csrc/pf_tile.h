@@ -35,7 +35,10 @@
 #pragma once
 
 #define PF_TS 16   // series per tile (MFMA N)
-#define PF_TNW 4   // waves per tile workgroup
+#define PF_TNW 4   // waves per tile workgroup (one per SIMD; 8 waves, two per SIMD, measured
+                   // no faster: the row pass is bound by the SIMD's FP64 pipe, shared by
+                   // MFMA and VALU, and the register cap of two waves spills the step)
+#define PF_TSW 4   // waves that run the per-series phases (16 lanes per series)
 #define PF_TH 5    // L-BFGS history (Stan default)
 #define PF_TV 64   // LDS stride of a per-series parameter vector
 #define PF_TNP 4   // parameters per lane (p = g + 16 i)
@@ -109,6 +112,24 @@ __device__ __forceinline__ double grp_sum(double v) {
   return v;
 }
 
+// DPP row (16-lane) scans, zero fill at the row edge: inclusive prefix
+// (lane g: sum over g' <= g) and inclusive suffix (sum over g' >= g)
+#define PF_DPP_ROWBCAST(n) (0x150 + (n))  // row_newbcast: lane n of each row
+__device__ __forceinline__ double row_prefix(double v) {
+  v += dpp_f64<PF_DPP_SHR(1)>(v);
+  v += dpp_f64<PF_DPP_SHR(2)>(v);
+  v += dpp_f64<PF_DPP_SHR(4)>(v);
+  v += dpp_f64<PF_DPP_SHR(8)>(v);
+  return v;
+}
+__device__ __forceinline__ double row_suffix(double v) {
+  v += dpp_f64<PF_DPP_SHL(1)>(v);
+  v += dpp_f64<PF_DPP_SHL(2)>(v);
+  v += dpp_f64<PF_DPP_SHL(4)>(v);
+  v += dpp_f64<PF_DPP_SHL(8)>(v);
+  return v;
+}
+
 typedef double TVec[PF_TNP];
 
 __device__ __forceinline__ double tvdot(const TVec &u, const TVec &v) {
@@ -137,20 +158,29 @@ template <int MODE>
 __device__ __forceinline__ void tile_publish(const FitKArgs &a, TileSmem<MODE> &sm, int j, int g) {
   const int S = a.S, K = a.K;
   const double *x = sm.xq + (size_t)j * PF_TV;
+  // segment tables k_s = k + sum_{c < s} delta_c, m_s = m - sum_{c < s}
+  // t_c delta_c: row-parallel inclusive prefix (lane g: changepoints g and
+  // g + 16; the 16 lanes of series j are one DPP row).  Flat growth: k = 0
+  // and no slope changes (trend = m).
+  const bool lin = a.growth == PF_GROWTH_LINEAR;
+  const double k = lin ? x[0] : 0.0, m = x[1];
+  const double da = (lin && g < S) ? x[2 + g] : 0.0, db = (lin && g + 16 < S) ? x[18 + g] : 0.0;
+  double pa = da, qa = sm.ctc[g] * da, pb = db, qb = sm.ctc[g + 16] * db;
+  pa = row_prefix(pa);
+  qa = row_prefix(qa);
+  pb = row_prefix(pb) + dpp_f64<PF_DPP_ROWBCAST(15)>(pa);
+  qb = row_prefix(qb) + dpp_f64<PF_DPP_ROWBCAST(15)>(qa);
   if (g == 0) {
-    // flat growth: k = 0 and no slope changes in the tables (trend = m)
-    const bool lin = a.growth == PF_GROWTH_LINEAR;
-    const double k = lin ? x[0] : 0.0, m = x[1];
-    double cd = 0.0, ctd = 0.0;
     sm.kseg[j * PF_TSEG] = k;
     sm.mseg[j * PF_TSEG] = m;
-    for (int jj = 0; jj < S; ++jj) {
-      const double d = lin ? x[2 + jj] : 0.0;
-      cd += d;
-      ctd = fma(sm.ctc[jj], d, ctd);
-      sm.kseg[j * PF_TSEG + jj + 1] = k + cd;
-      sm.mseg[j * PF_TSEG + jj + 1] = m - ctd;
-    }
+  }
+  if (g < S) {
+    sm.kseg[j * PF_TSEG + g + 1] = k + pa;
+    sm.mseg[j * PF_TSEG + g + 1] = m - qa;
+  }
+  if (g + 16 < S) {
+    sm.kseg[j * PF_TSEG + g + 17] = k + pb;
+    sm.mseg[j * PF_TSEG + g + 17] = m - qb;
   }
   if (g == 1) {
     const double sg = exp(x[2 + S]);
@@ -189,13 +219,11 @@ template <int MODE>
 __device__ __forceinline__ void tile_rows(const FitKArgs &a, TileSmem<MODE> &sm, int tile, int n) {
   constexpr int NSET = TileSmem<MODE>::NSET;
   constexpr bool HM = (MODE & 3) != MODE_ADD, HA = (MODE & 3) != MODE_MULT;
-  const int lane = pf_lane(), wave = pf_wave();
+  const int lane = pf_lane(), wave = __builtin_amdgcn_readfirstlane(pf_wave());
   const int T = a.T, Tp = a.Tp;
   const int j = lane & 15, rq = lane >> 4;
   const int s_g = tile * PF_TS + j;
   const bool svalid = s_g < n;
-  const double *ys = a.y_scaled + (size_t)(svalid ? s_g : 0) * Tp;
-  const double *XR = a.XR;
   const double *kseg = sm.kseg + j * PF_TSEG, *mseg = sm.mseg + j * PF_TSEG;
   const int jrow = 4 * (j & 3) + (j >> 2);
   // B operands of Xb: k-step kk, lane k index rq <-> feature 8 rq + kk
@@ -205,23 +233,37 @@ __device__ __forceinline__ void tile_rows(const FitKArgs &a, TileSmem<MODE> &sm,
     bmr[kk] = HM ? sm.bm[(8 * rq + kk) * PF_TS + j] : 0.0;
     bar_[kk] = HA ? sm.ba[(8 * rq + kk) * PF_TS + j] : 0.0;
   }
-  // unconditional wide loads (T_pad % 128 == 0 keeps every chunk row in
-  // range; XR is zero past K): no predicated load to drain the prefetch
+  // Chunk loads as buffer loads: lane-constant byte offsets (voffset) plus
+  // the chunk's uniform offset (soffset), no per-load address arithmetic;
+  // unconditional (T_pad % 128 == 0 keeps every chunk row in range, XR is
+  // zero past K, rows of series past n read 0 from the y buffer's range
+  // check), so no predicated load drains the prefetch.
+  const int nvalid = min(n - tile * PF_TS, PF_TS);
+  const __amdgpu_buffer_rsrc_t rXR = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<double *>(a.XR), (short)0, Tp * 32 * 8, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rT = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<double *>(a.t), (short)0, Tp * 8, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rS = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<int32_t *>(a.seg), (short)0, Tp * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rY = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<double *>(a.y_scaled + (size_t)tile * PF_TS * Tp), (short)0, nvalid * Tp * 8,
+      0x00020000);
+  const int oxa = (jrow * 32 + 8 * rq) * 8, oxg = (4 * rq * 32 + 2 * j) * 8;
+  const int ot = 4 * rq * 8, oy = (j * Tp + 4 * rq) * 8, os = 4 * rq * 4;
+  auto ld2 = [](__amdgpu_buffer_rsrc_t r, int vo, int so) {
+    return __builtin_bit_cast(pf_d2, __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, 0));
+  };
   auto tload = [&](int c, TileIn &in) {
     const int r0 = 16 * c;
-    const pf_d2 *xa = reinterpret_cast<const pf_d2 *>(XR + (size_t)(r0 + jrow) * 32 + 8 * rq);
 #pragma unroll
-    for (int h = 0; h < 4; ++h) in.xa[h] = xa[h];
-    const pf_d2 *xg = reinterpret_cast<const pf_d2 *>(XR + (size_t)(r0 + 4 * rq) * 32 + 2 * j);
+    for (int h = 0; h < 4; ++h) in.xa[h] = ld2(rXR, oxa + 16 * h, r0 * 256);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) in.xg[q] = xg[q * 16];
-    const pf_d2 *tt = reinterpret_cast<const pf_d2 *>(a.t + r0 + 4 * rq);
-    const pf_d2 *yy = reinterpret_cast<const pf_d2 *>(ys + r0 + 4 * rq);
-    in.t[0] = tt[0];
-    in.t[1] = tt[1];
-    in.y[0] = yy[0];
-    in.y[1] = yy[1];
-    in.sg = *reinterpret_cast<const pf_i4 *>(a.seg + r0 + 4 * rq);
+    for (int q = 0; q < 4; ++q) in.xg[q] = ld2(rXR, oxg + 256 * q, r0 * 256);
+    in.t[0] = ld2(rT, ot, r0 * 8);
+    in.t[1] = ld2(rT, ot + 16, r0 * 8);
+    in.y[0] = ld2(rY, oy, r0 * 8);
+    in.y[1] = ld2(rY, oy + 16, r0 * 8);
+    in.sg = __builtin_bit_cast(pf_i4, __builtin_amdgcn_raw_buffer_load_b128(rS, os, r0 * 4, 0));
   };
   auto xb_mfma = [&](const TileIn &in, pf_d4 &xm, pf_d4 &xa) {
     // two independent accumulation chains per product (even / odd k-steps)
@@ -256,10 +298,11 @@ __device__ __forceinline__ void tile_rows(const FitKArgs &a, TileSmem<MODE> &sm,
   };
   const int nch = (T + 15) >> 4;
   const int c0 = (nch * wave) / PF_TNW, c1 = (nch * (wave + 1)) / PF_TNW;
-  // one chunk: loads of chunk c + 2 into `nn`, Xb of chunk c + 1 (`nx`) on
-  // the matrix pipe, then chunk c's (`cu`, Xb in `xc`) elementwise work and
-  // X'W.  Input and Xb buffers rotate three ways: no register copies of
-  // in-flight loads or MFMA results.
+  // one chunk: loads of chunk c + 2 into `nn`, Xb of chunk c + 1 (`nx`)
+  // issued before chunk c's (`cu`, Xb in `xc`) elementwise work and X'W.
+  // Input and Xb buffers rotate three ways: no register copies of in-flight
+  // loads or MFMA results.  (A four-buffer ring, loads three chunks ahead,
+  // measured no faster.)
   auto step = [&](int c, const TileIn &cu, const TileIn &nx, TileIn &nn, const pf_d4 &xcm,
                   const pf_d4 &xca, pf_d4 &xnm, pf_d4 &xna) {
     const int r0 = 16 * c;
@@ -364,12 +407,30 @@ __device__ __forceinline__ bool tile_assemble(const FitKArgs &a, TileSmem<MODE> 
   const double *pk = sm.pk + (size_t)j * PF_TV;
   const double sigma = sm.sig[2 * j], inv = sm.sig[2 * j + 1], tau = a.tau;
   const double rrt = sm.rr[j];
-  // segment totals: lane g holds segments g and g + 16 (S + 1 <= 32)
+  // segment sums, lane g: segments g and g + 16 (S + 1 <= 32).  Suffix
+  // sums over segments by a DPP row scan; changepoint jj is active in the
+  // segments s > jj, so parameter p = 2 + jj needs the suffix at s = p - 1:
+  // lane g - 1 of the same half (row_shr:1), or row lane 15 across halves.
   const double s0a = (g <= S) ? sm.sg0[g * PF_TS + j] : 0.0;
   const double s1a = (g <= S) ? sm.sg1[g * PF_TS + j] : 0.0;
   const double s0b = (g + 16 <= S) ? sm.sg0[(g + 16) * PF_TS + j] : 0.0;
   const double s1b = (g + 16 <= S) ? sm.sg1[(g + 16) * PF_TS + j] : 0.0;
-  const double tot0 = grp_sum(s0a + s0b), tot1 = grp_sum(s1a + s1b);
+  const double u0b = row_suffix(s0b), u1b = row_suffix(s1b);
+  const double u0a = row_suffix(s0a) + dpp_f64<PF_DPP_ROWBCAST(0)>(u0b);
+  const double u1a = row_suffix(s1a) + dpp_f64<PF_DPP_ROWBCAST(0)>(u1b);
+  const double tot0 = dpp_f64<PF_DPP_ROWBCAST(0)>(u0a), tot1 = dpp_f64<PF_DPP_ROWBCAST(0)>(u1a);
+  double su0[3], su1[3];
+  {
+    const double h0a = dpp_f64<PF_DPP_SHR(1)>(u0a), h1a = dpp_f64<PF_DPP_SHR(1)>(u1a);
+    const double h0b = dpp_f64<PF_DPP_SHR(1)>(u0b), h1b = dpp_f64<PF_DPP_SHR(1)>(u1b);
+    const double e0a = dpp_f64<PF_DPP_ROWBCAST(15)>(u0a), e1a = dpp_f64<PF_DPP_ROWBCAST(15)>(u1a);
+    su0[0] = h0a;
+    su1[0] = h1a;
+    su0[1] = g == 0 ? e0a : h0b;
+    su1[1] = g == 0 ? e1a : h1b;
+    su0[2] = dpp_f64<PF_DPP_ROWBCAST(15)>(u0b);
+    su1[2] = dpp_f64<PF_DPP_ROWBCAST(15)>(u1b);
+  }
   double fl = 0.0, gp = 0.0;
   bool bad = false;
 #pragma unroll
@@ -387,13 +448,8 @@ __device__ __forceinline__ bool tile_assemble(const FitKArgs &a, TileSmem<MODE> 
     } else if (p < 2 + S) {
       // changepoint jj is active in segments s > jj
       const int jj = p - 2;
-      double su0 = 0.0, su1 = 0.0;
-      for (int s = jj + 1; s <= S; ++s) {
-        su0 += sm.sg0[s * PF_TS + j];
-        su1 += sm.sg1[s * PF_TS + j];
-      }
       const double sgn = (xv > 0.0) - (xv < 0.0);
-      gv = (linear ? -inv * (su1 - sm.ctc[jj] * su0) : 0.0) + sgn / tau;
+      gv = (linear ? -inv * (su1[i < 3 ? i : 2] - sm.ctc[jj] * su0[i < 3 ? i : 2]) : 0.0) + sgn / tau;
       ft = fabs(xv) / tau;
     } else if (p == 2 + S) {
       gv = (double)T - inv * rrt + 4.0 * sigma * sigma;
@@ -683,9 +739,10 @@ __global__ __launch_bounds__(PF_TNW * 64, 1) void k_fit_tile(FitKArgs a, int n) 
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   TileSmem<MODE> sm;
   sm.carve(smem_raw);
-  const int tile = blockIdx.x, lane = pf_lane(), wave = pf_wave();
+  const int tile = blockIdx.x, lane = pf_lane(), wave = __builtin_amdgcn_readfirstlane(pf_wave());
   const int P = a.P, S = a.S;
-  const int j = 4 * wave + (lane >> 4), g = lane & 15;  // series j's 16 lanes
+  const bool stepper = wave < PF_TSW;                   // per-series phases: waves 0..3
+  const int j = (4 * wave + (lane >> 4)) & 15, g = lane & 15;  // series j's 16 lanes
   const int sgl = tile * PF_TS + j;
   const bool warm = a.warm_cap != 0;
   const pf_fit_opts o = a.o;
@@ -698,7 +755,7 @@ __global__ __launch_bounds__(PF_TNW * 64, 1) void k_fit_tile(FitKArgs a, int n) 
     sm.csa[i] = (i < a.K) ? a.s_a[i] : 0.0;
   }
   for (int e = threadIdx.x; e < NACC; e += PF_TNW * 64) sm.gb[e] = 0.0;
-  {
+  if (stepper) {
     TileZ &z = sm.z[j];
     const bool live = sgl < n && a.status[sgl] != PF_ST_CONSTANT;
     double *xq = sm.xq + (size_t)j * PF_TV, *xk = sm.xk + (size_t)j * PF_TV;
@@ -714,7 +771,7 @@ __global__ __launch_bounds__(PF_TNW * 64, 1) void k_fit_tile(FitKArgs a, int n) 
     }
   }
   __syncthreads();
-  tile_publish<MODE>(a, sm, j, g);
+  if (stepper) tile_publish<MODE>(a, sm, j, g);
   __syncthreads();
   while (true) {
     PF_STAMP(0);
@@ -723,29 +780,32 @@ __global__ __launch_bounds__(PF_TNW * 64, 1) void k_fit_tile(FitKArgs a, int n) 
     __syncthreads();
     PF_STAMP(2);
     PF_COUNT(7);
-    TileZ &z = sm.z[j];
-    double fq, gpq;
-    const bool bad = tile_assemble<MODE>(a, sm, j, g, fq, gpq);
+    double fq = 0.0, gpq = 0.0;
+    bool bad = false;
+    if (stepper) bad = tile_assemble<MODE>(a, sm, j, g, fq, gpq);
     PF_STAMP(3);
     __syncthreads();       // every wave has read the accumulators
     for (int e = threadIdx.x; e < NACC; e += PF_TNW * 64) sm.gb[e] = 0.0;
-    bool need = false;
-    TileZ zl = z;          // group-local copy; lane g == 0 writes it back
-    if (!zl.done) {
-      zl.fq = fq;
-      zl.gpq = gpq;
-      zl.bad = bad ? 1 : 0;
-      zl.n_eval++;
-      need = tile_lbfgs<MODE>(o, sm, zl, j, g, P);
-      if (!need) zl.done = 1;
+    if (stepper) {
+      TileZ &z = sm.z[j];
+      bool need = false;
+      TileZ zl = z;        // group-local copy; lane g == 0 writes it back
+      if (!zl.done) {
+        zl.fq = fq;
+        zl.gpq = gpq;
+        zl.bad = bad ? 1 : 0;
+        zl.n_eval++;
+        need = tile_lbfgs<MODE>(o, sm, zl, j, g, P);
+        if (!need) zl.done = 1;
+      }
+      PF_STAMP(4);
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      if (g == 0) z = zl;
+      if (need) tile_publish<MODE>(a, sm, j, g);
+      const unsigned long long any = __ballot(need);
+      if (lane == 0) sm.flag[wave] = any != 0ull ? 1 : 0;
     }
-    PF_STAMP(4);
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    if (g == 0) z = zl;
-    if (need) tile_publish<MODE>(a, sm, j, g);
-    const unsigned long long any = __ballot(need);
-    if (lane == 0) sm.flag[wave] = any != 0ull ? 1 : 0;
     PF_STAMP(5);
     __syncthreads();
     PF_STAMP(6);
@@ -753,7 +813,7 @@ __global__ __launch_bounds__(PF_TNW * 64, 1) void k_fit_tile(FitKArgs a, int n) 
     if (!__builtin_amdgcn_readfirstlane(more)) break;
   }
   // outputs (pass-0 semantics of fit_body)
-  if (sgl < n) {
+  if (stepper && sgl < n) {
     const TileZ &z = sm.z[j];
     double *th = a.theta + (size_t)sgl * P;
     const int st_in = a.status[sgl];
