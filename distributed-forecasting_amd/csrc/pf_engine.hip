@@ -1705,6 +1705,8 @@ struct PredKArgs {
   const uint32_t *series_id;  // RNG stream key per series (NULL: batch index)
   int method;                 // PF_INTERVAL_EXACT / PF_INTERVAL_SAMPLE
   const double *cap;          // [n][Tp] logistic capacity / y_scale on the predicted rows
+  float zthr;                 // deterministic-trend rows: tail threshold on the standard
+                              // normal draws (0: always the general selection)
 };
 
 // numpy _lerp: a + (b-a)*t, or b - (b-a)*(1-t) when t >= 0.5
@@ -2401,6 +2403,21 @@ int pf_predict(pf_ctx *ctx, const pf_predict_args *p, void *stream) {
     a.k_hi_neg = a.N - 2 - khi;
     a.fr_hi = (float)(ihi - khi);
     if (a.N == 1) { a.k_lo = 0; a.fr_lo = 0.f; a.k_hi_neg = 0; a.fr_hi = 0.f; }
+    // threshold selection on the normal draws of deterministic-trend rows
+    // (k_predict_mc): z* with N Phi(-z*) = k + 22 expected keys beyond it —
+    // exact whenever between k + 2 and 64 keys fall beyond (else the
+    // general selection runs): ~99% of rows at N = 1000
+    a.zthr = 0.0f;
+    const int kmax = a.k_lo > a.k_hi_neg ? a.k_lo : a.k_hi_neg;
+    if (a.N >= 200 && kmax + 22 <= 60 && !getenv_flag("PF_MC_GENERAL_SELECT")) {
+      const double target = (double)(kmax + 22) / (double)a.N;  // tail mass
+      double lo = 0.0, hi = 10.0;
+      for (int it = 0; it < 80; ++it) {
+        const double mid = 0.5 * (lo + hi);
+        if (0.5 * erfc(mid / sqrt(2.0)) > target) lo = mid; else hi = mid;
+      }
+      a.zthr = (float)(0.5 * (lo + hi));
+    }
   }
   a.method = p->interval_method;
   a.cap = p->cap_scaled;
@@ -2415,7 +2432,16 @@ int pf_predict(pf_ctx *ctx, const pf_predict_args *p, void *stream) {
   if (a.N > 0) {
     // exact mode: one block (PF_MC_WAVES waves) per series over the random
     // rows (the horizon); sample mode: every row, <= 64 rows per wave
-    const int gx = (a.method == PF_INTERVAL_SAMPLE) ? (a.Tf + 64 * PF_MC_WAVES - 1) / (64 * PF_MC_WAVES) : 1;
+    // sample mode: every row; a block per (series, row range) while the
+    // batch is small, one block per series (its per-sample changepoint setup
+    // done once) when the series alone fill the GPU
+    int gx = 1;
+    if (a.method == PF_INTERVAL_SAMPLE) {
+      gx = (a.Tf + 64 * PF_MC_WAVES - 1) / (64 * PF_MC_WAVES);
+      const int want = (8192 + a.n_series - 1) / a.n_series;  // blocks per series for ~8k blocks
+      if (gx > want) gx = want;
+      if (gx < 1) gx = 1;
+    }
     const dim3 gmc(gx, a.n_series);
     PF_TIMED_LAUNCH(ctx, "k_predict_mc", gmc.x * gmc.y, (hipStream_t)stream,
                     (k_predict_mc<64>), gmc, dim3(PF_MC_WAVES * 64), 0, (hipStream_t)stream, a);

@@ -143,6 +143,57 @@ __device__ __forceinline__ void wave_tail_select(const float (&v)[PF_NQ], const 
   }
 }
 
+// inclusive prefix sum of an int across the wave
+__device__ __forceinline__ int wave_prefix_i32(int v) {
+  v += dpp_i32<PF_DPP_SHR(1)>(v);
+  v += dpp_i32<PF_DPP_SHR(2)>(v);
+  v += dpp_i32<PF_DPP_SHR(4)>(v);
+  v += dpp_i32<PF_DPP_SHR(8)>(v);
+  v += dpp_i32<PF_DPP_BCAST15, 0xA>(v);
+  v += dpp_i32<PF_DPP_BCAST31, 0xC>(v);
+  return v;
+}
+
+// Deterministic-trend rows: the samples are yhat + sd z with z standard
+// normal, a monotone map, so the order statistics are those of z.  Ranks
+// kk[0], kk[0]+1 of z (lower tail) and kk[1], kk[1]+1 of -z (upper tail)
+// from the keys beyond the fixed threshold zthr: exact when each tail holds
+// between kk + 2 and 64 keys (returns false otherwise: the caller runs the
+// general wave_tail_select).  Absent samples are NaN (never beyond).
+__device__ __forceinline__ bool wave_tail_select_z(const float (&z)[PF_NQ], const int (&kk)[2], float zthr,
+                                                   float *buf, float (&o0)[2], float (&o1)[2]) {
+  const int lane = pf_lane();
+  int c0 = 0, c1 = 0;
+#pragma unroll
+  for (int q = 0; q < PF_NQ; ++q) {
+    c0 += (z[q] < -zthr) ? 1 : 0;
+    c1 += (z[q] > zthr) ? 1 : 0;
+  }
+  const int p0 = wave_prefix_i32(c0), p1 = wave_prefix_i32(c1);
+  const int M0 = __builtin_amdgcn_readlane(p0, 63), M1 = __builtin_amdgcn_readlane(p1, 63);
+  if (M0 < kk[0] + 2 || M0 > 64 || M1 < kk[1] + 2 || M1 > 64) return false;
+  int w0 = p0 - c0, w1 = 64 + p1 - c1;
+#pragma unroll
+  for (int q = 0; q < PF_NQ; ++q) {
+    if (z[q] < -zthr) buf[w0++] = z[q];
+    if (z[q] > zthr) buf[w1++] = -z[q];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  float c[2];
+  c[0] = (lane < M0) ? buf[lane] : INFINITY;
+  c[1] = (lane < M1) ? buf[64 + lane] : INFINITY;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  wave_sort_asc_n(c);
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    o0[s] = readlane_f32(c[s], kk[s]);
+    o1[s] = readlane_f32(c[s], kk[s] + 1);
+  }
+  return true;
+}
+
 // sample smp's c-th new changepoint: tau = t_c - 1 ~ U(0, T - 1], delta ~ Laplace(0, lam)
 __device__ __forceinline__ void mc_sample_cp(uint32_t seed0, uint32_t seed1, uint32_t series, int smp,
                                              int c, double t_max, double lam, double &tau, double &dl) {
@@ -330,6 +381,7 @@ __device__ __forceinline__ void mc_rows(const PredKArgs &a, const PredSeries &ps
         }
       }
       PF_STAMP1(5);
+      float zs[PF_NQ];
 #pragma unroll
       for (int c = 0; c < PF_NQ / 4; ++c) {
         const pf_u4 rr = philox4x32_10(pf_u4{(uint32_t)c, (uint32_t)lane, (uint32_t)row, sid},
@@ -341,11 +393,20 @@ __device__ __forceinline__ void mc_rows(const PredKArgs &a, const PredSeries &ps
         for (int j = 0; j < 4; ++j) {
           const int q = 4 * c + j;
           v[q] = random ? fmaf(sd, z[j], fmaf(tv[q], u1, addf)) : fmaf(sd, z[j], yh);
-          if (lane + 64 * q >= N) v[q] = __builtin_nanf("");
+          zs[q] = z[j];
+          if (lane + 64 * q >= N) {
+            v[q] = __builtin_nanf("");
+            zs[q] = __builtin_nanf("");
+          }
         }
       }
       PF_STAMP1(6);
-      if (random) {
+      float zo0[2], zo1[2];
+      if (!random && a.zthr > 0.0f && wave_tail_select_z(zs, kk2, a.zthr, buf, zo0, zo1)) {
+        // order statistics of yhat + sd z: the same monotone map of z's
+        ylo = np_lerp(fmaf(sd, zo0[0], yh), fmaf(sd, zo1[0], yh), a.fr_lo);
+        yhi = np_lerp(fmaf(sd, -zo1[1], yh), fmaf(sd, -zo0[1], yh), a.fr_hi);
+      } else if (random) {
         float o0[4], o1[4];
         wave_tail_select<4>(v, tv, kk4, buf, o0, o1);
         if (N == 1) { for (int s = 0; s < 4; ++s) o1[s] = o0[s]; }

@@ -179,6 +179,29 @@ def test_intervals_within_mc_error(eng, golden_ref, method):
         assert np.allclose(tlo[:1826], thi[:1826], rtol=0, atol=1e-4 * ysc[s])
 
 
+@pytest.mark.parametrize("n_samples", [1000, 300])
+def test_sample_mode_threshold_selection_is_exact(eng, golden_ref, monkeypatch, n_samples):
+    """k_predict_mc selects the order statistics of deterministic-trend rows
+    from the normal draws beyond a fixed threshold (falling back to the
+    general wave selection when a tail holds too few or too many keys): the
+    same order statistics, so the sample-mode output is bitwise that of the
+    general selection (PF_MC_GENERAL_SELECT=1) on every row, history and
+    horizon."""
+    ds, Y, fut = golden_ref["ds_ns"], golden_ref["Y"], golden_ref["fut_ns"]
+    g = _grid(eng, ds)
+    fit = eng.fit(g, _Y(g, Y))
+    fg = eng.predict_grid(fit, fut)
+    res = {}
+    for general in (False, True):
+        if general:
+            monkeypatch.setenv("PF_MC_GENERAL_SELECT", "1")
+        out = eng.predict(fit, fg, n_samples=n_samples, seed=5, interval_method="sample")
+        res[general] = {k: out[k][:, :fg.T].cpu().numpy() for k in ("yhat_lower", "yhat_upper",
+                                                                     "trend_lower", "trend_upper")}
+    for k in res[False]:
+        assert np.array_equal(res[False][k], res[True][k]), k
+
+
 @pytest.mark.parametrize("method", ["exact", "sample"])
 def test_interval_coverage_history(eng, golden_ref, method):
     ds, Y = golden_ref["ds_ns"], golden_ref["Y"]

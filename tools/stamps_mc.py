@@ -8,7 +8,10 @@ _lib.load(os.path.abspath("distributed-forecasting_amd/libprophet_hip_stamps.so"
 import distributed_forecasting_amd as dfa
 from distributed_forecasting_amd import synthetic, batch as B
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 500
-ds = synthetic.daily_dates(); Y = synthetic.sales_matrix(n, ds)
+method = sys.argv[2] if len(sys.argv) > 2 else "exact"        # "sample": configs[3]'s literal loop
+cfg = int(sys.argv[3]) if len(sys.argv) > 3 else 1              # 3: 730-day configs[3] shape
+ds = synthetic.daily_dates() if cfg != 3 else synthetic.daily_dates("2016-01-01", "2017-12-30")
+Y = synthetic.sales_matrix(n, ds, config_index=cfg)
 eng = dfa.Engine(0)
 seasons = eng.config.seasons(int(ds[0]), int(ds[-1]), int(ds[1] - ds[0]))
 grid = dfa.build_grid(ds, seasons, start_ns=int(ds[0]), t_scale_ns=int(ds[-1] - ds[0]))
@@ -17,7 +20,7 @@ fit = eng.fit(grid, Yd)
 fg = eng.predict_grid(fit, B.future_dates(ds, 90))
 buf = (ctypes.c_ulonglong * 32)()
 torch.cuda.synchronize(); _lib._lib.pf_debug_stamps(buf, 1)
-eng.predict(fit, fg, seed=1); torch.cuda.synchronize()
+eng.predict(fit, fg, seed=1, interval_method=method); torch.cuda.synchronize()
 _lib._lib.pf_debug_stamps(buf, 1)
 v = np.array(list(buf), dtype=np.float64)
 rows = max(v[9], 1)
