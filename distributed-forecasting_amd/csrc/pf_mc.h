@@ -382,13 +382,31 @@ __device__ __forceinline__ void mc_rows(const PredKArgs &a, const PredSeries &ps
       }
       PF_STAMP1(5);
       float zs[PF_NQ];
+      // the lane's 16 noise draws: 16 uniforms of 24 bits from 12 Philox
+      // words (three calls; each word's top 24 bits, the fourth uniform of a
+      // group from the three low bytes), Box-Muller pairs
+      uint32_t uw[PF_NQ];
+#pragma unroll
+      for (int c = 0; c < PF_NQ / 4; c += 1) {
+        if (c < 3) {
+          const pf_u4 rr = philox4x32_10(pf_u4{(uint32_t)c, (uint32_t)lane, (uint32_t)row, sid},
+                                         a.seed0, a.seed1);
+          const uint32_t w[4] = {rr.x, rr.y, rr.z, rr.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            // words 4c + j, c < 3: groups g = (4c + j) / 3 of three words
+            const int wi = 4 * c + j, g = wi / 3, m = wi % 3;
+            uw[4 * g + m] = w[j];
+            if (m == 0) uw[4 * g + 3] = (w[j] & 0xFFu) << 8;
+            else uw[4 * g + 3] |= (w[j] & 0xFFu) << (8 + 8 * m);
+          }
+        }
+      }
 #pragma unroll
       for (int c = 0; c < PF_NQ / 4; ++c) {
-        const pf_u4 rr = philox4x32_10(pf_u4{(uint32_t)c, (uint32_t)lane, (uint32_t)row, sid},
-                                       a.seed0, a.seed1);
         float z[4];
-        pf_box_muller(pf_u01f(rr.x), pf_u01f(rr.y), z[0], z[1]);
-        pf_box_muller(pf_u01f(rr.z), pf_u01f(rr.w), z[2], z[3]);
+        pf_box_muller(pf_u01f(uw[4 * c]), pf_u01f(uw[4 * c + 1]), z[0], z[1]);
+        pf_box_muller(pf_u01f(uw[4 * c + 2]), pf_u01f(uw[4 * c + 3]), z[2], z[3]);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int q = 4 * c + j;
