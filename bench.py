@@ -357,6 +357,7 @@ def main():
                                max_over_ranks, sum_over_ranks, timed, parallel, device)
         res["configs2_strong"] = configs2(args, eng, ds, seasons, fut, rank, world, device, timed,
                                           sum_over_ranks, parallel, B, diagnostics, dfa)
+        res["ragged"] = ragged_leg(args, eng, device, timed, sum_over_ranks, B, dfa)
 
     if cpu is not None:
         m = cpu["n"]
@@ -500,6 +501,82 @@ def configs2(args, eng, ds, seasons, fut, rank, world, device, timed, sum_over_r
             "note": "configs[2]: 50k synthetic daily series x 1826 days (config_index 2) in total, "
                     "splitmix64((store << 32) | item) mod N shards, fit + 90-day forecast + "
                     "1000-sample intervals + metrics + RCCL all-gather per step"}
+
+
+def ragged_leg(args, eng, device, timed, sum_over_ranks, B, dfa):
+    """A staggered store-item table (each series its own launch date, two end
+    dates: ~100 distinct date grids over 500 series) with inputs resident in
+    HBM: one ragged launch per kernel (engine.RaggedGrid) vs one launch per
+    distinct grid (the bucket path), each step = grids + fit + 90-day forecast
+    with intervals."""
+    import torch
+    from distributed_forecasting_amd import engine as E, synthetic, training
+    df = synthetic.staggered_frame(10, args.series_per_gpu // 10, n_starts=50, n_ends=2,
+                                   max_delay_days=730)
+    gkeys, rows = training.group_frame(df, ["store", "item"])
+    ds_all = B.to_ns(df["ds"])
+    y = df["y"].to_numpy(np.float64)
+    bks = B.bucket_groups([ds_all[r] for r in rows], [y[r] for r in rows])
+    packs = B.ragged_packs(bks, eng.config)
+    assert len(packs) == 1
+    cfg = eng.config
+    dev = int(device.index)
+    Tp = E.pad_rows(max(bk.fit_ds.shape[0] for bk in bks))
+    sizes = [bk.Y.shape[0] for bk in bks]
+    row0 = np.concatenate(([0], np.cumsum(sizes)))
+    n = int(row0[-1])
+    Yh = np.zeros((n, Tp))
+    for j, bk in enumerate(bks):
+        Yh[row0[j]:row0[j + 1], :bk.fit_ds.shape[0]] = bk.Y
+    Yd = torch.from_numpy(Yh).to(device)
+    pkeys = np.concatenate([gkeys[bk.members] for bk in bks])
+    sid = torch.from_numpy(B.series_id(pkeys)).to(device)
+    gof = np.repeat(np.arange(len(bks)), sizes)
+    futs = [B.future_dates(bk.history_dates, HORIZON) for bk in bks]
+    spec = []
+    for bk in bks:
+        f = bk.fit_ds
+        spec.append((f, cfg.seasons(int(f[0]), int(f[-1]), B.min_positive_diff(f)), int(f[0]),
+                     int(f[-1] - f[0])))
+
+    def grid(j, T_pad=None):
+        f, se, st, sc = spec[j]
+        return dfa.build_grid(f, se, start_ns=st, t_scale_ns=sc, device=dev, T_pad=T_pad)
+
+    fds = [s[0] for s in spec]
+    st0 = [s[2] for s in spec]
+    sc0 = [s[3] for s in spec]
+
+    def one_launch():
+        rg = E.RaggedGrid.build(fds, spec[0][1], st0, sc0, gof, device=dev, T_pad=Tp)
+        fit = eng.fit(rg, Yd)
+        fg = eng.predict_grid(fit, futs)
+        return fit, eng.predict(fit, fg, seed=0, components=False, series_id=sid)
+
+    def per_bucket():
+        fits = []
+        for j in range(len(bks)):
+            sl = slice(int(row0[j]), int(row0[j + 1]))
+            g = grid(j)
+            Yj = torch.zeros((sizes[j], g.T_pad), dtype=torch.float64, device=device)
+            Yj[:, :g.T] = Yd[sl, :g.T]
+            fit = eng.fit(g, Yj)
+            fg = eng.predict_grid(fit, futs[j])
+            fits.append(eng.predict(fit, fg, seed=0, components=False, series_id=sid[sl]))
+        return fits
+    steps = args.dropin_steps
+    el, ka, (fit, _) = timed(one_launch, steps)
+    el_b, ka_b, _ = timed(per_bucket, steps)
+    tot = sum_over_ranks(n)
+    return {"value": tot * steps / el, "unit": "series/s", "ms_per_step": el / steps * 1e3,
+            "kernels_ms": ka, "n_series": n, "n_grids": len(bks),
+            "T_min": int(min(s[0].shape[0] for s in spec)), "T_max": int(Tp and max(s[0].shape[0] for s in spec)),
+            "map_certified": float((fit.status == 70).float().mean().item()),
+            "per_bucket_launches": {"value": tot * steps / el_b, "ms_per_step": el_b / steps * 1e3,
+                                    "kernels_ms": ka_b},
+            "note": "staggered table (synthetic.staggered_frame: 50 launch dates over 730 days, 2 "
+                    "end dates): every kernel launched once for all grids (ragged) vs once per "
+                    "distinct grid; inputs resident, grids + fit + forecast + intervals per step"}
 
 
 def torch_zeros_like_grid(Y, device):

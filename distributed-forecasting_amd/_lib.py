@@ -22,7 +22,7 @@ PF_ST_CONSTANT = 50
 EXPORTED = ["pf_ctx_create", "pf_ctx_destroy", "pf_last_error", "pf_default_fit_opts",
             "pf_num_changepoints", "pf_build_grid", "pf_prepare", "pf_objective_grad",
             "pf_fit", "pf_predict", "pf_set_timing", "pf_read_timings", "pf_cv_metrics",
-            "pf_hessian"]
+            "pf_hessian", "pf_prepare_ragged", "pf_build_grids"]
 PF_MAX_COMP = 32  # include/prophet_hip.h
 PF_INTERVAL = {"exact": 0, "sample": 1}
 CV_METRICS = ["mse", "rmse", "mae", "mape", "smape", "coverage", "mdape"]
@@ -50,7 +50,8 @@ class PfProblem(ctypes.Structure):
                 ("grid", PfGrid),
                 ("sigmas", vp), ("s_a", vp), ("s_m", vp), ("y_scaled", vp), ("cap_scaled", vp),
                 ("fourier_orders", i32 * 3), ("season_mode", i32),
-                ("tau_series", vp), ("sigmas_series", vp)]
+                ("tau_series", vp), ("sigmas_series", vp),
+                ("n_grids", i32), ("grids", vp), ("grid_of", vp)]
 
 
 class PfFitOpts(ctypes.Structure):
@@ -70,7 +71,8 @@ class PfPredictArgs(ctypes.Structure):
                 ("trend", vp), ("trend_lower", vp), ("trend_upper", vp),
                 ("mult_terms", vp), ("add_terms", vp),
                 ("n_comp", i32), ("comp_col0", i32 * PF_MAX_COMP), ("comp_ncol", i32 * PF_MAX_COMP), ("comp", vp),
-                ("series_id", vp)]
+                ("series_id", vp),
+                ("n_grids", i32), ("grids", vp), ("grid_of", vp)]
 
 
 class PfCvArgs(ctypes.Structure):
@@ -112,6 +114,11 @@ def load(path: str = LIB_PATH):
                                   vp, vp, vp, vp, vp, vp, ctypes.c_int, vp]
     lib.pf_prepare.argtypes = [vp, ctypes.c_int, ctypes.POINTER(PfGrid), ctypes.c_int,
                                vp, vp, vp, vp, vp, vp, vp, vp]
+    lib.pf_build_grids.argtypes = [vp, ctypes.c_int, vp, vp, ctypes.c_int, ctypes.c_int,
+                                   ctypes.POINTER(PfSeason), ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_double, vp, vp, vp, vp, vp, vp, ctypes.c_int, vp, vp]
+    lib.pf_prepare_ragged.argtypes = [vp, ctypes.c_int, ctypes.POINTER(PfGrid), ctypes.c_int,
+                                      vp, vp, ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.pf_objective_grad.argtypes = [vp, ctypes.POINTER(PfProblem), vp, vp, vp, vp]
     lib.pf_hessian.argtypes = [vp, ctypes.POINTER(PfProblem), vp, vp, vp]
     lib.pf_fit.argtypes = [vp, ctypes.POINTER(PfProblem), ctypes.POINTER(PfFitOpts),

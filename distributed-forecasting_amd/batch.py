@@ -136,6 +136,32 @@ def bucket_groups(ds_list, y_list) -> list:
             for fds, hd, ys, mem in parts]
 
 
+def ragged_packs(buckets, config) -> list:
+    """Group buckets (lists of bucket indices) whose grids can share one
+    ragged launch: the same seasonalities under UPSTREAM's auto rules on each
+    bucket's own history span and the same number of changepoints.  Staggered
+    launch dates, gaps and different end dates then cost one launch per pack
+    instead of one per distinct date set (02_training.py:277-307: every
+    (store, item) group brings its own history)."""
+    from . import _lib as L
+    key_to_pack, packs = {}, []
+    for b, bk in enumerate(buckets):
+        fds = bk.fit_ds
+        if fds.shape[0] < 2 or int(fds[-1] - fds[0]) <= 0:
+            key = ("single", b)        # fit_dense raises Prophet's error for it
+        else:
+            seasons = config.seasons(int(fds[0]), int(fds[-1]), min_positive_diff(fds))
+            S = max(1, L.num_changepoints(fds.shape[0], config.n_changepoints,
+                                          config.changepoint_range))
+            key = (tuple(seasons), S)
+        p = key_to_pack.get(key)
+        if p is None:
+            key_to_pack[key] = p = len(packs)
+            packs.append([])
+        packs[p].append(b)
+    return packs
+
+
 # ---------------------------------------------------------------------------
 # fitted batch
 # ---------------------------------------------------------------------------
@@ -342,3 +368,107 @@ class FittedBatch:
                           engine.config)
         sid = rec["series_id"][sel] if "series_id" in rec else None
         return cls(engine, fit, rec["history_dates"], None, sid)
+
+
+class RaggedFittedBatch:
+    """Series of several buckets (different date grids) fitted and forecast
+    in single launches: one sub-grid per bucket, shared row stride, the
+    kernels bind each workgroup to its series' grid (engine.RaggedGrid).
+    Rows are the buckets' series in bucket order."""
+
+    def __init__(self, engine: E.Engine, fit: E.FitResult, buckets, series_ids=None):
+        self.engine = engine
+        self.fit = fit
+        self.buckets = list(buckets)
+        sizes = [int(bk.Y.shape[0]) for bk in self.buckets]
+        self.row0 = np.concatenate(([0], np.cumsum(sizes))).astype(np.int64)
+        self.series_ids = None
+        if series_ids is not None:
+            self.series_ids = torch.from_numpy(np.ascontiguousarray(series_ids, dtype=np.int32)) \
+                .to(fit.theta.device)
+
+    @property
+    def n(self) -> int:
+        return int(self.fit.theta.shape[0])
+
+    @classmethod
+    def fit_buckets(cls, engine: E.Engine, buckets, series_ids=None, polish: bool | None = None,
+                    cap=None) -> "RaggedFittedBatch":
+        """Fit every series of ``buckets`` (each: fit_ds, history_dates, Y
+        [n_b, T_b]) in one launch.  ``cap`` (logistic growth): a list with one
+        [n_b, T_b] array per bucket."""
+        cfg = engine.config
+        dev = torch.device("cuda", engine.device)
+        Tp = E.pad_rows(max(int(bk.fit_ds.shape[0]) for bk in buckets))
+        starts, scales, seasons = [], [], None
+        for bk in buckets:
+            fds = np.asarray(bk.fit_ds, np.int64)
+            if fds.shape[0] < 2:
+                raise ValueError("Dataframe has less than 2 non-NaN rows.")
+            start, t_scale = int(fds[0]), int(fds[-1] - fds[0])
+            if t_scale <= 0:
+                raise ValueError("history must span more than one distinct date")
+            se = cfg.seasons(start, int(fds[-1]), min_positive_diff(fds))
+            if seasons is not None and se != seasons:
+                raise ValueError("ragged buckets must share their seasonalities (ragged_packs)")
+            seasons = se
+            starts.append(start)
+            scales.append(t_scale)
+        sizes = [int(bk.Y.shape[0]) for bk in buckets]
+        rg = E.RaggedGrid.build([bk.fit_ds for bk in buckets], seasons, starts, scales,
+                                np.repeat(np.arange(len(buckets)), sizes), device=engine.device,
+                                T_pad=Tp, n_changepoints=cfg.n_changepoints,
+                                changepoint_range=cfg.changepoint_range)
+        n = int(sum(sizes))
+        Yh = np.zeros((n, Tp), np.float64)
+        caph = np.zeros((n, Tp), np.float64) if cfg.growth == "logistic" else None
+        if cfg.growth == "logistic" and cap is None:
+            raise ValueError('Capacities must be supplied for logistic growth in column "cap"')
+        r = 0
+        for b, bk in enumerate(buckets):
+            T = int(bk.fit_ds.shape[0])
+            Yh[r:r + sizes[b], :T] = bk.Y
+            if caph is not None:
+                caph[r:r + sizes[b], :T] = cap[b]
+            r += sizes[b]
+        Yd = E._to_device_async(Yh, dev)
+        capd = E._to_device_async(caph, dev) if caph is not None else None
+        fit = engine.fit(rg, Yd, polish=polish, cap=capd)
+        return cls(engine, fit, buckets, series_ids)
+
+    def future(self, periods: int, freq="D", include_history: bool = True) -> list:
+        """UPSTREAM make_future_dataframe per bucket (its own last date)."""
+        return [future_dates(bk.history_dates, periods, freq, include_history=include_history)
+                for bk in self.buckets]
+
+    def predict(self, ds_list, *, seed: int = 0, n_samples: int | None = None,
+                components: bool = True, cap=None):
+        """Forecast every series on its bucket's dates (``ds_list[b]``, sorted)
+        in one launch.  Returns (Tf per bucket, dict of float32 device tensors
+        [n, T_pad]; row i valid up to its bucket's Tf).  ``cap`` (logistic):
+        a list with one [n_b, Tf_b] array per bucket."""
+        eng = self.engine
+        fg = eng.predict_grid(self.fit, [np.asarray(d, np.int64) for d in ds_list])
+        capd = None
+        if eng.config.growth == "logistic":
+            if cap is None:
+                raise ValueError('Capacities must be supplied for logistic growth in column "cap"')
+            ch = np.zeros((self.n, fg.T_pad), np.float64)
+            for b in range(len(self.buckets)):
+                c = np.asarray(cap[b], np.float64)
+                ch[self.row0[b]:self.row0[b + 1], :c.shape[1]] = c
+            capd = torch.from_numpy(ch).to(self.fit.theta.device)
+        out = eng.predict(self.fit, fg, n_samples=n_samples, seed=seed, components=components,
+                          series_id=self.series_ids, cap=capd)
+        return [len(d) for d in ds_list], out
+
+    def sub_batch(self, b: int) -> FittedBatch:
+        """Bucket b's series as a plain FittedBatch on its own grid (the
+        params-store unit; no copy of the fit beyond row views)."""
+        sl = slice(int(self.row0[b]), int(self.row0[b + 1]))
+        f = self.fit
+        sub = E.FitResult(f.grid.grids[b], f.theta[sl], f.y_scale[sl], f.f[sl], f.f_stan[sl],
+                          f.status[sl], f.n_iter[sl], f.n_eval[sl], f.config)
+        bk = self.buckets[b]
+        sid = self.series_ids[sl].cpu().numpy() if self.series_ids is not None else None
+        return FittedBatch(self.engine, sub, bk.history_dates, bk.fit_ds, sid)

@@ -326,3 +326,11 @@ __device__ __forceinline__ uint32_t pf_f2ord(float f) {
 __device__ __forceinline__ float pf_ord2f(uint32_t o) {
   return __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
 }
+
+// uniform pointer (both halves from the first active lane: kept in SGPRs)
+__device__ __forceinline__ const void *rfl_ptr(const void *p) {
+  const uint64_t v = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (const void *)(((uint64_t)hi << 32) | lo);
+}

@@ -135,20 +135,20 @@ struct SeasonSpec {
 // d = (ns / 1e9) / 86400  (pandas total_seconds()/(3600*24.));
 // X col (2i, 2i+1) = sin, cos of ((2.0*(i+1))*pi*d)/period evaluated
 // left to right like UPSTREAM fourier_series.
-__global__ void k_grid_features(const int64_t *__restrict__ ds, int T, int Tp, int64_t start,
-                                int64_t tscale, SeasonSpec ss, const double *__restrict__ extra,
-                                int n_extra, double *__restrict__ t_out, double *__restrict__ XT) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= Tp) return;
+__device__ __forceinline__ void grid_features_row(int i, bool valid, int64_t ns, int Tp,
+                                                  int64_t start, int64_t tscale,
+                                                  const SeasonSpec &ss,
+                                                  const double *__restrict__ extra, int n_extra,
+                                                  int T, double *__restrict__ t_out,
+                                                  double *__restrict__ XT) {
   int col = 0;
-  if (i >= T) {
+  if (!valid) {
     if (t_out) t_out[i] = 0.0;
     for (int b = 0; b < ss.n; ++b)
       for (int r = 0; r < 2 * ss.order[b]; ++r) XT[(size_t)(col++) * Tp + i] = 0.0;
     for (int e = 0; e < n_extra; ++e) XT[(size_t)(col++) * Tp + i] = 0.0;
     return;
   }
-  const int64_t ns = ds[i];
   if (t_out) t_out[i] = __ddiv_rn((double)(ns - start), (double)tscale);
   const double d = __ddiv_rn(__ddiv_rn((double)ns, 1e9), 86400.0);
   for (int b = 0; b < ss.n; ++b) {
@@ -164,11 +164,36 @@ __global__ void k_grid_features(const int64_t *__restrict__ ds, int T, int Tp, i
   for (int e = 0; e < n_extra; ++e) XT[(size_t)(col++) * Tp + i] = extra[(size_t)e * T + i];
 }
 
+__global__ void k_grid_features(const int64_t *__restrict__ ds, int T, int Tp, int64_t start,
+                                int64_t tscale, SeasonSpec ss, const double *__restrict__ extra,
+                                int n_extra, double *__restrict__ t_out, double *__restrict__ XT) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= Tp) return;
+  grid_features_row(i, i < T, i < T ? ds[i] : 0, Tp, start, tscale, ss, extra, n_extra, T, t_out, XT);
+}
+
+// Ragged design builder (pf_build_grids): grid g = blockIdx.y, its parameters
+// prm[g*6 ..] = {ds offset, T, start, t_scale, first, step}; dates first +
+// i*step when step > 0 (generated here), else ds[offset + i].
+__global__ void k_grids_features(const int64_t *__restrict__ prm, const int64_t *__restrict__ ds,
+                                 int Tp, int K, SeasonSpec ss, double *__restrict__ t_out,
+                                 double *__restrict__ XT) {
+  const int g = blockIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= Tp) return;
+  const int64_t *p = prm + (size_t)g * 6;
+  const int T = (int)p[1];
+  const int64_t step = p[5];
+  int64_t ns = 0;
+  if (i < T) ns = step > 0 ? p[4] + (int64_t)i * step : ds[p[0] + i];
+  grid_features_row(i, i < T, ns, Tp, p[2], p[3], ss, nullptr, 0, T, t_out + (size_t)g * Tp,
+                    XT + (size_t)g * K * Tp);
+}
+
 // UPSTREAM set_changepoints: linspace(0, hist_size-1, n_cp+1).round()[1:]
 // (numpy: step = (stop-start)/div; y = arange*step; y[-1] = stop; rint)
-__global__ void k_grid_changepoints(const double *__restrict__ t, int T, int n_cp_req, double range,
-                                    double *__restrict__ t_change, int32_t *__restrict__ cp_idx) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+__device__ void grid_changepoints(const double *__restrict__ t, int T, int n_cp_req, double range,
+                                  double *__restrict__ t_change, int32_t *__restrict__ cp_idx) {
   const int hist_size = (int)floor((double)T * range);
   int n_cp = n_cp_req;
   if (n_cp + 1 > hist_size) n_cp = hist_size - 1;
@@ -193,13 +218,27 @@ __global__ void k_grid_changepoints(const double *__restrict__ t, int T, int n_c
     cp_idx[0] = -1;
   }
 }
+__global__ void k_grid_changepoints(const double *__restrict__ t, int T, int n_cp_req, double range,
+                                    double *__restrict__ t_change, int32_t *__restrict__ cp_idx) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  grid_changepoints(t, T, n_cp_req, range, t_change, cp_idx);
+}
+// ragged: one thread per grid (grid g's t at t + g*Tp, S slots per grid)
+__global__ void k_grids_changepoints(const int64_t *__restrict__ prm, int G, int Tp, int S,
+                                     int n_cp_req, double range, const double *__restrict__ t,
+                                     double *__restrict__ t_change, int32_t *__restrict__ cp_idx) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  grid_changepoints(t + (size_t)g * Tp, (int)prm[(size_t)g * 6 + 1], n_cp_req, range,
+                    t_change + (size_t)g * S, cp_idx + (size_t)g * S);
+}
 
 // seg[i] = #{j : t_change[j] <= t[i]} (Stan A[i,j] = t_i >= t_change_j);
 // cp_first[j] = first row with t >= t_change[j].
-__global__ void k_grid_segments(const double *__restrict__ t, int T, int Tp,
-                                const double *__restrict__ t_change, int S,
-                                int32_t *__restrict__ seg, int32_t *__restrict__ cp_first) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void grid_segments(int i, const double *__restrict__ t, int T, int Tp,
+                                              const double *__restrict__ t_change, int S,
+                                              int32_t *__restrict__ seg,
+                                              int32_t *__restrict__ cp_first) {
   if (i < Tp) {
     int c = S;
     if (i < T) {
@@ -219,6 +258,35 @@ __global__ void k_grid_segments(const double *__restrict__ t, int T, int Tp,
     cp_first[i] = lo;
   }
 }
+__global__ void k_grid_segments(const double *__restrict__ t, int T, int Tp,
+                                const double *__restrict__ t_change, int S,
+                                int32_t *__restrict__ seg, int32_t *__restrict__ cp_first) {
+  grid_segments(blockIdx.x * blockDim.x + threadIdx.x, t, T, Tp, t_change, S, seg, cp_first);
+}
+// ragged: grid g = blockIdx.y; also writes grid g's pf_grid descriptor
+__global__ void k_grids_segments(const int64_t *__restrict__ prm, int Tp, int K, int S,
+                                 const double *__restrict__ t, const double *__restrict__ XT,
+                                 const double *__restrict__ t_change, int32_t *__restrict__ seg,
+                                 int32_t *__restrict__ cp_first, pf_grid *__restrict__ desc) {
+  const int g = blockIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int T = (int)prm[(size_t)g * 6 + 1];
+  grid_segments(i, t + (size_t)g * Tp, T, Tp, t_change + (size_t)g * S, S, seg + (size_t)g * Tp,
+                cp_first + (size_t)g * S);
+  if (desc && i == 0) {
+    pf_grid d;
+    d.T = T;
+    d.T_pad = Tp;
+    d.K = K;
+    d.S = S;
+    d.t = t + (size_t)g * Tp;
+    d.XT = XT + (size_t)g * K * Tp;
+    d.t_change = t_change + (size_t)g * S;
+    d.seg = seg + (size_t)g * Tp;
+    d.cp_first = cp_first + (size_t)g * S;
+    desc[g] = d;
+  }
+}
 
 // ============================================================================
 // prepare: y_scale, y_scaled, init (UPSTREAM initialize_scales, *_growth_init)
@@ -230,9 +298,17 @@ __global__ __launch_bounds__(256) void k_prepare(int T, int Tp, const double *__
                                                  double *__restrict__ y_scaled,
                                                  double *__restrict__ cap_scaled,
                                                  double *__restrict__ theta0,
-                                                 int32_t *__restrict__ status, int P, int S) {
+                                                 int32_t *__restrict__ status, int P, int S,
+                                                 const pf_grid *__restrict__ grids,
+                                                 const int32_t *__restrict__ grid_of) {
   __shared__ double red[3][4];
   const int s = blockIdx.x;
+  if (grid_of) {
+    // ragged batch: this series' own rows and t
+    const int g = __builtin_amdgcn_readfirstlane(grid_of[s]);
+    T = __builtin_amdgcn_readfirstlane(grids[g].T);
+    t = (const double *)rfl_ptr(grids[g].t);
+  }
   const double *ys = y + (size_t)s * Tp;
   double amax = 0.0, vmin = INFINITY, vmax = -INFINITY, vsum = 0.0;
   for (int i = threadIdx.x; i < T; i += blockDim.x) {
@@ -359,7 +435,36 @@ struct FitKArgs {
   pf_fit_opts o;
   int pass;      // 0: first L-BFGS pass; >0: resume series the polish did not certify
   int warm_cap;  // this pass's iteration cap is the warm-up cap (MAXIT -> WARMUP)
+  // ragged batch (pf_problem.grids): series s fits on grids[grid_of[s]]; that
+  // grid's lane-blocked copy sits at rg_base + g * rg_stride bytes (same
+  // layout as tP / XTP / sgP with the grid's own R, TQ); NULL: one grid
+  const pf_grid *grids;
+  const int32_t *grid_of;
+  const char *rg_base;
+  size_t rg_stride;
 };
+
+
+// Ragged batch: point the grid fields of `a` at series s's own grid (uniform
+// per workgroup).  Rows owned per thread R = ceil(T / NL) as for a batch of
+// that grid alone, so a series fitted in a ragged batch follows the same
+// arithmetic as in a batch of its own grid.
+template <int NL>
+__device__ __forceinline__ void bind_grid(FitKArgs &a, int s) {
+  const int g = __builtin_amdgcn_readfirstlane(a.grid_of[s]);
+  const pf_grid *G = a.grids + g;
+  a.T = __builtin_amdgcn_readfirstlane(G->T);
+  a.t = (const double *)rfl_ptr(G->t);
+  a.XT = (const double *)rfl_ptr(G->XT);
+  a.t_change = (const double *)rfl_ptr(G->t_change);
+  a.seg = (const int32_t *)rfl_ptr(G->seg);
+  a.R = (a.T + NL - 1) / NL;
+  a.TQ = NL * a.R;
+  const double *base = (const double *)(a.rg_base + (size_t)g * a.rg_stride);
+  a.tP = base;
+  a.XTP = base + a.TQ;
+  a.sgP = (const int32_t *)(base + (size_t)a.TQ * (1 + a.K));
+}
 
 // Generated Fourier block: harmonics r >= 1 from the first harmonic column
 // pair by the angle-addition recurrence (|err| ~ r ulp), so a pass reads two
@@ -994,7 +1099,9 @@ __device__ __forceinline__ void load_y(const FitKArgs &a, FitSmem<NW, KMAX, MODE
 
 // ---------------------------------------------------------------- K2 kernel
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
-__global__ __launch_bounds__(NW * 64) void k_objgrad(FitKArgs a) {
+__global__ __launch_bounds__(NW * 64) void k_objgrad(FitKArgs a0) {
+  FitKArgs a = a0;
+  if (a0.grid_of) bind_grid<NW * 64>(a, blockIdx.x);
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   FitSmem<NW, KMAX, MODE> sm;
   sm.carve(smem_raw, a.TQ, a.P);
@@ -1598,7 +1705,9 @@ __device__ __forceinline__ void polish_body(const FitKArgs &a) {
 // Exact Hessian of the smooth part at theta (pf_hessian; the polish's model
 // without damping): H_out[s][P][P].
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
-__global__ __launch_bounds__(NW * 64) void k_hessian(FitKArgs a, double *H_out) {
+__global__ __launch_bounds__(NW * 64) void k_hessian(FitKArgs a0, double *H_out) {
+  FitKArgs a = a0;
+  if (a0.grid_of) bind_grid<NW * 64>(a, blockIdx.x);
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   FitSmem<NW, KMAX, MODE> sm;
   sm.carve(smem_raw, a.TQ, a.P);
@@ -1635,19 +1744,27 @@ struct FitOcc {
   static constexpr int W = KMAX > 34 ? 1 : 2;
 };
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
-__global__ __launch_bounds__(NW * 64, FitOcc<KMAX>::W) void k_fit(FitKArgs a) {
+__global__ __launch_bounds__(NW * 64, FitOcc<KMAX>::W) void k_fit(FitKArgs a0) {
+  FitKArgs a = a0;
+  if (a0.grid_of) bind_grid<NW * 64>(a, blockIdx.x);
   fit_body<NW, KMAX, O0, O1, O2, MODE>(a, a.pass, a.o, a.warm_cap != 0);
 }
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
-__global__ __launch_bounds__(NW * 64, FitOcc<KMAX>::W) void k_fit_resume(FitKArgs a) {
+__global__ __launch_bounds__(NW * 64, FitOcc<KMAX>::W) void k_fit_resume(FitKArgs a0) {
+  FitKArgs a = a0;
+  if (a0.grid_of) bind_grid<NW * 64>(a, blockIdx.x);
   fit_body<NW, KMAX, O0, O1, O2, MODE>(a, a.pass, a.o, a.warm_cap != 0);
 }
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
-__global__ __launch_bounds__(NW * 64, FitOcc<KMAX>::W) void k_polish(FitKArgs a) {
+__global__ __launch_bounds__(NW * 64, FitOcc<KMAX>::W) void k_polish(FitKArgs a0) {
+  FitKArgs a = a0;
+  if (a0.grid_of) bind_grid<NW * 64>(a, blockIdx.x);
   polish_body<NW, KMAX, O0, O1, O2, MODE>(a);
 }
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
-__global__ __launch_bounds__(NW * 64, FitOcc<KMAX>::W) void k_polish_resume(FitKArgs a) {
+__global__ __launch_bounds__(NW * 64, FitOcc<KMAX>::W) void k_polish_resume(FitKArgs a0) {
+  FitKArgs a = a0;
+  if (a0.grid_of) bind_grid<NW * 64>(a, blockIdx.x);
   polish_body<NW, KMAX, O0, O1, O2, MODE>(a);
 }
 // The warm-up hand-off of launch_fitlike — L-BFGS warm-up -> polish, once
@@ -1670,7 +1787,7 @@ __device__ __noinline__ void polish_phase(const FitKArgs &a) {
   polish_body<NW, KMAX, O0, O1, O2, MODE>(a);
 }
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
-__global__ __launch_bounds__(NW * 64, FitOcc<KMAX>::W) void k_fit_polish(FitKArgs a) {
+__device__ __forceinline__ void fit_polish_passes(const FitKArgs &a) {
   const int W = a.o.lbfgs_warmup;
   for (int ps = 0; ps < 3; ++ps) {
     const bool warm = ps < 2;
@@ -1680,6 +1797,17 @@ __global__ __launch_bounds__(NW * 64, FitOcc<KMAX>::W) void k_fit_polish(FitKArg
     __syncthreads();
     const int st = __builtin_amdgcn_readfirstlane(__atomic_load_n(&a.status[blockIdx.x], __ATOMIC_RELAXED));
     if (st == PF_ST_MAP || st == PF_ST_CONSTANT || st == PF_ST_BADINIT) break;
+  }
+}
+template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
+__global__ __launch_bounds__(NW * 64, FitOcc<KMAX>::W) void k_fit_polish(FitKArgs a) {
+  if (a.grid_of) {
+    // ragged batch: the phases read this series' grid from a private copy
+    FitKArgs b = a;
+    bind_grid<NW * 64>(b, blockIdx.x);
+    fit_polish_passes<NW, KMAX, O0, O1, O2, MODE>(b);
+  } else {
+    fit_polish_passes<NW, KMAX, O0, O1, O2, MODE>(a);
   }
 }
 
@@ -1707,7 +1835,21 @@ struct PredKArgs {
   const double *cap;          // [n][Tp] logistic capacity / y_scale on the predicted rows
   float zthr;                 // deterministic-trend rows: tail threshold on the standard
                               // normal draws (0: always the general selection)
+  const pf_grid *grids;       // ragged forecasts: series s predicts on grids[grid_of[s]]
+  const int32_t *grid_of;     // (NULL: every series on t / XT / seg above)
 };
+
+// Ragged forecast: rows / t / features / segments / changepoints of series s's
+// own forecast grid (uniform per workgroup).
+__device__ __forceinline__ void bind_pred_grid(PredKArgs &a, int s) {
+  const int g = __builtin_amdgcn_readfirstlane(a.grid_of[s]);
+  const pf_grid *G = a.grids + g;
+  a.Tf = __builtin_amdgcn_readfirstlane(G->T);
+  a.t = (const double *)rfl_ptr(G->t);
+  a.XT = (const double *)rfl_ptr(G->XT);
+  a.t_change = (const double *)rfl_ptr(G->t_change);
+  a.seg = (const int32_t *)rfl_ptr(G->seg);
+}
 
 // numpy _lerp: a + (b-a)*t, or b - (b-a)*(1-t) when t >= 0.5
 __device__ __forceinline__ float np_lerp(float a, float b, float t) {
@@ -1781,9 +1923,11 @@ __device__ __forceinline__ double pred_trend(const PredKArgs &a, const PredSerie
 // the interval endpoints of deterministic rows are exact order-statistic
 // draws (pf_ostat.h); rows left to k_predict_mc are not written here.
 template <int KMAX>
-__global__ __launch_bounds__(256) void k_predict_det(PredKArgs a) {
+__global__ __launch_bounds__(256) void k_predict_det(PredKArgs a0) {
   __shared__ PredSeries ps;
   const int series = blockIdx.y;
+  PredKArgs a = a0;
+  if (a0.grid_of) bind_pred_grid(a, series);
   const uint32_t sid = a.series_id ? a.series_id[series] : (uint32_t)series;
   pred_setup(a, series, ps);
   __syncthreads();
@@ -1993,20 +2137,75 @@ int pf_build_grid(pf_ctx *ctx, const int64_t *ds_ns, int T, int T_pad, int64_t s
   return 0;
 }
 
-int pf_prepare(pf_ctx *ctx, int n_series, const pf_grid *grid, int growth, const double *y,
-               const double *cap, double *y_scale, double *y_scaled, double *cap_scaled,
-               double *theta0, int32_t *status, void *stream) {
+int pf_build_grids(pf_ctx *ctx, int n_grids, const int64_t *grid_params, const int64_t *ds_ns,
+                   int T_max, int T_pad, const pf_season *seasons_host, int n_season,
+                   int n_changepoints, double changepoint_range, double *t_out, double *XT_out,
+                   double *t_change_io, int32_t *cp_idx_out, int32_t *seg_out,
+                   int32_t *cp_first_out, int S, pf_grid *grids_out, void *stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (n_grids < 0) return set_err(ctx, "pf_build_grids: n_grids < 0");
+  if (n_grids == 0) return 0;
+  if (T_max < 1 || T_pad < T_max || (T_pad % 128) != 0) return set_err(ctx, "pf_build_grids: bad T_max/T_pad");
+  if (n_season < 0 || n_season > PF_MAX_SEASONS) return set_err(ctx, "pf_build_grids: n_season");
+  if (!grid_params || !t_out || !XT_out || !t_change_io || !seg_out || !cp_first_out || !grids_out)
+    return set_err(ctx, "pf_build_grids: NULL buffer");
+  if (n_changepoints >= 0 && !cp_idx_out) return set_err(ctx, "pf_build_grids: cp_idx_out NULL");
+  if (S < 1) return set_err(ctx, "pf_build_grids: S must be >= 1");
+  SeasonSpec ss;
+  ss.n = n_season;
+  int K = 0;
+  for (int b = 0; b < n_season; ++b) {
+    ss.period[b] = seasons_host[b].period;
+    ss.order[b] = seasons_host[b].order;
+    K += 2 * ss.order[b];
+  }
+  if (K < 1) return set_err(ctx, "pf_build_grids: no seasonality columns");
+  const int nb = (T_pad + 255) / 256;
+  PF_TIMED_LAUNCH(ctx, "k_grids_features", nb * n_grids, st, k_grids_features, dim3(nb, n_grids),
+                  dim3(256), 0, st, grid_params, ds_ns, T_pad, K, ss, t_out, XT_out);
+  PF_HIP(ctx, hipGetLastError());
+  if (n_changepoints >= 0) {
+    const int nc = (n_grids + 63) / 64;
+    PF_TIMED_LAUNCH(ctx, "k_grids_changepoints", nc, st, k_grids_changepoints, dim3(nc), dim3(64),
+                    0, st, grid_params, n_grids, T_pad, S, n_changepoints, changepoint_range,
+                    t_out, t_change_io, cp_idx_out);
+    PF_HIP(ctx, hipGetLastError());
+  }
+  const int ns = ((T_pad > S ? T_pad : S) + 255) / 256;
+  PF_TIMED_LAUNCH(ctx, "k_grids_segments", ns * n_grids, st, k_grids_segments, dim3(ns, n_grids),
+                  dim3(256), 0, st, grid_params, T_pad, K, S, t_out, XT_out, t_change_io, seg_out,
+                  cp_first_out, grids_out);
+  PF_HIP(ctx, hipGetLastError());
+  return 0;
+}
+
+int pf_prepare_ragged(pf_ctx *ctx, int n_series, const pf_grid *grid, int n_grids,
+                      const pf_grid *grids_dev, const int32_t *grid_of, int growth,
+                      const double *y, const double *cap, double *y_scale, double *y_scaled,
+                      double *cap_scaled, double *theta0, int32_t *status, void *stream) {
   if (n_series < 0 || !grid || !y || !y_scale || !y_scaled || !theta0 || !status)
     return set_err(ctx, "pf_prepare: bad arguments");
+  if (n_grids < 0 || (n_grids > 0 && (!grids_dev || !grid_of)))
+    return set_err(ctx, "pf_prepare_ragged: n_grids > 0 needs grids and grid_of");
+  if (n_grids == 0 && !grid->t) return set_err(ctx, "pf_prepare: NULL grid.t");
+  if (grid->T < 2 || grid->T > grid->T_pad) return set_err(ctx, "pf_prepare: bad T / T_pad");
   if (growth == PF_GROWTH_LOGISTIC && (!cap || !cap_scaled))
     return set_err(ctx, "pf_prepare: logistic growth needs cap and cap_scaled");
   if (n_series == 0) return 0;
   const int P = 3 + grid->S + grid->K;
   PF_TIMED_LAUNCH(ctx, "k_prepare", n_series, (hipStream_t)stream, k_prepare, dim3(n_series),
                   dim3(256), 0, (hipStream_t)stream, grid->T, grid->T_pad, grid->t, growth, y,
-                  cap, y_scale, y_scaled, cap_scaled, theta0, status, P, grid->S);
+                  cap, y_scale, y_scaled, cap_scaled, theta0, status, P, grid->S,
+                  n_grids > 0 ? grids_dev : nullptr, n_grids > 0 ? grid_of : nullptr);
   PF_HIP(ctx, hipGetLastError());
   return 0;
+}
+
+int pf_prepare(pf_ctx *ctx, int n_series, const pf_grid *grid, int growth, const double *y,
+               const double *cap, double *y_scale, double *y_scaled, double *cap_scaled,
+               double *theta0, int32_t *status, void *stream) {
+  return pf_prepare_ragged(ctx, n_series, grid, 0, nullptr, nullptr, growth, y, cap, y_scale,
+                           y_scaled, cap_scaled, theta0, status, stream);
 }
 
 }  // extern "C"
@@ -2026,6 +2225,32 @@ __global__ __launch_bounds__(256) void k_permute_grid(const double *__restrict__
   const int TQ = NL * R;
   const int q = blockIdx.x * 256 + threadIdx.x;
   if (q >= TQ) return;
+  const int r = q / NL, L = q - r * NL;
+  const int i = L * R + r;
+  const bool v = i < T;
+  tP[q] = v ? t[i] : 0.0;
+  const int sg = v ? seg[i] : S;
+  const int sp = v ? (i > 0 ? seg[i - 1] : 0) : S;
+  sgP[q] = sg | ((sg - sp) << 16);
+  for (int f = 0; f < K; ++f) XTP[(size_t)f * TQ + q] = v ? XT[(size_t)f * Tp + i] : 0.0;
+}
+
+// Ragged batch: the lane-blocked copy of every grid (blockIdx.y = grid), each
+// with its own R = ceil(T / NL), at base + g * stride bytes.
+__global__ __launch_bounds__(256) void k_permute_grid_ragged(const pf_grid *__restrict__ grids,
+                                                             int Tp, int K, int S, int NL,
+                                                             char *__restrict__ base, size_t stride) {
+  const int g = blockIdx.y;
+  const int T = __builtin_amdgcn_readfirstlane(grids[g].T);
+  const int R = (T + NL - 1) / NL, TQ = NL * R;
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  if (q >= TQ) return;
+  const double *__restrict__ t = grids[g].t;
+  const int32_t *__restrict__ seg = grids[g].seg;
+  const double *__restrict__ XT = grids[g].XT;
+  double *tP = (double *)(base + (size_t)g * stride);
+  double *XTP = tP + TQ;
+  int32_t *sgP = (int32_t *)(tP + (size_t)TQ * (1 + K));
   const int r = q / NL, L = q - r * NL;
   const int i = L * R + r;
   const bool v = i < T;
@@ -2073,6 +2298,10 @@ FitKArgs make_fit_args(const pf_problem *pb) {
   a.sigmas_series = pb->sigmas_series;
   a.y_scaled = pb->y_scaled;
   a.cap_scaled = pb->cap_scaled;
+  if (pb->n_grids > 0) {
+    a.grids = pb->grids;
+    a.grid_of = pb->grid_of;
+  }
   return a;
 }
 
@@ -2135,6 +2364,7 @@ int launch_fitlike(pf_ctx *ctx, int what, const FitKArgs &a, int n, hipStream_t 
       smem_t = TileSmem<MODE>::bytes();
       tile = a.o.tile_min_series >= 0 && n >= a.o.tile_min_series && a.P <= PF_TV && a.K <= 32 &&
              a.S + 1 <= 32 && a.growth != PF_GROWTH_LOGISTIC && !a.tau_series && !a.sigmas_series && a.XR &&
+             !a.grid_of &&
              smem_t <= 160 * 1024;
     }
     if (npass == 3 && !tile && !getenv_flag("PF_SPLIT_POLISH")) {
@@ -2235,10 +2465,28 @@ extern "C" {
 
 // Context scratch for one fit-like call: [lane-blocked grid | polish rows],
 // then the permutation launch (stream-ordered with the fit that reads it).
-static int prepare_fit_scratch(pf_ctx *ctx, FitKArgs &a, hipStream_t st, bool rowmajor = false) {
+static int prepare_fit_scratch(pf_ctx *ctx, FitKArgs &a, hipStream_t st, bool rowmajor = false,
+                               int n_grids = 0) {
   const size_t TQ = (size_t)a.TQ;
   size_t gbytes = TQ * sizeof(double) * (1 + (size_t)a.K) + TQ * sizeof(int32_t);
   gbytes = (gbytes + 255) & ~(size_t)255;
+  if (a.grid_of) {
+    // ragged: one lane-blocked copy per grid (envelope-sized slots)
+    void *w = nullptr;
+    const int rc = ctx_workspace(ctx, gbytes * (size_t)n_grids, &w);
+    if (rc) return rc;
+    a.rg_base = (const char *)w;
+    a.rg_stride = gbytes;
+    a.tP = a.XTP = nullptr;
+    a.sgP = nullptr;
+    a.XR = nullptr;
+    const int nb = (int)((TQ + 255) / 256);
+    PF_TIMED_LAUNCH(ctx, "k_permute_grid_ragged", nb * n_grids, st, k_permute_grid_ragged,
+                    dim3(nb, n_grids), dim3(256), 0, st, a.grids, a.Tp, a.K, a.S, PF_FIT_NW * 64,
+                    (char *)w, gbytes);
+    PF_HIP(ctx, hipGetLastError());
+    return 0;
+  }
   const size_t rbytes = rowmajor ? (size_t)a.Tp * 32 * sizeof(double) : 0;
   void *w = nullptr;
   const int rc = ctx_workspace(ctx, gbytes + rbytes, &w);
@@ -2276,9 +2524,13 @@ static int check_problem(pf_ctx *ctx, const pf_problem *pb) {
   const int P = 3 + pb->grid.S + pb->grid.K;
   if (P > 128) return set_err(ctx, "P = 3 + S + K must be <= 128");
   if (pb->grid.S < 1 || pb->grid.S > 62) return set_err(ctx, "S out of range");
-  if (pb->grid.T < 2 || pb->grid.T_pad % 128) return set_err(ctx, "bad T / T_pad");
-  if (!pb->grid.t || !pb->grid.XT || !pb->grid.t_change || !pb->grid.seg || !pb->sigmas ||
-      !pb->s_a || !pb->s_m || !pb->y_scaled)
+  if (pb->grid.T < 2 || pb->grid.T_pad % 128 || pb->grid.T > pb->grid.T_pad)
+    return set_err(ctx, "bad T / T_pad");
+  if (pb->n_grids < 0 || (pb->n_grids > 0 && (!pb->grids || !pb->grid_of)))
+    return set_err(ctx, "n_grids > 0 needs grids and grid_of");
+  if (pb->n_grids == 0 && (!pb->grid.t || !pb->grid.XT || !pb->grid.t_change || !pb->grid.seg))
+    return set_err(ctx, "NULL grid buffer in problem");
+  if (!pb->sigmas || !pb->s_a || !pb->s_m || !pb->y_scaled)
     return set_err(ctx, "NULL buffer in problem");
   return 0;
 }
@@ -2292,7 +2544,7 @@ int pf_objective_grad(pf_ctx *ctx, const pf_problem *pb, const double *theta, do
   a.theta = const_cast<double *>(theta);
   a.f_out = f;
   a.g_out = g;
-  rc = prepare_fit_scratch(ctx, a, (hipStream_t)stream);
+  rc = prepare_fit_scratch(ctx, a, (hipStream_t)stream, false, pb->n_grids);
   if (rc) return rc;
   return dispatch_fitlike(ctx, PF_LAUNCH_OBJGRAD, a, pb->n_series, pb->fourier_orders, mode_of(pb),
                           (hipStream_t)stream);
@@ -2316,8 +2568,8 @@ int pf_fit(pf_ctx *ctx, const pf_problem *pb, const pf_fit_opts *opts, double *t
   a.o = *opts;
   // the tiled first pass reads a row-major feature copy
   const bool maybe_tile = opts->tile_min_series >= 0 && pb->n_series >= opts->tile_min_series &&
-                          pb->grid.K <= 32;
-  rc = prepare_fit_scratch(ctx, a, (hipStream_t)stream, maybe_tile);
+                          pb->grid.K <= 32 && pb->n_grids == 0;
+  rc = prepare_fit_scratch(ctx, a, (hipStream_t)stream, maybe_tile, pb->n_grids);
   if (rc) return rc;
   return dispatch_fitlike(ctx, PF_LAUNCH_FIT, a, pb->n_series, pb->fourier_orders, mode_of(pb),
                           (hipStream_t)stream);
@@ -2330,7 +2582,7 @@ int pf_hessian(pf_ctx *ctx, const pf_problem *pb, const double *theta, double *H
   if (pb->n_series == 0) return 0;
   FitKArgs a = make_fit_args(pb);
   a.theta = const_cast<double *>(theta);
-  rc = prepare_fit_scratch(ctx, a, (hipStream_t)stream);
+  rc = prepare_fit_scratch(ctx, a, (hipStream_t)stream, false, pb->n_grids);
   if (rc) return rc;
   return dispatch_fitlike(ctx, PF_LAUNCH_HESSIAN, a, pb->n_series, pb->fourier_orders, mode_of(pb),
                           (hipStream_t)stream, H);
@@ -2341,8 +2593,12 @@ int pf_predict(pf_ctx *ctx, const pf_predict_args *p, void *stream) {
   if (p->n_samples < 0 || p->n_samples > 64 * PF_NQ) return set_err(ctx, "pf_predict: n_samples must be in [0, 1024]");
   const int P = 3 + p->fg.S + p->fg.K;
   if (P > 128 || p->fg.K > 64) return set_err(ctx, "pf_predict: P must be <= 128 and K <= 64");
-  if (!p->fg.t || !p->fg.XT || !p->fg.t_change || !p->fg.seg || !p->theta || !p->y_scale ||
-      !p->yhat || !p->yhat_lower || !p->yhat_upper)
+  if (p->n_grids < 0 || (p->n_grids > 0 && (!p->grids || !p->grid_of)))
+    return set_err(ctx, "pf_predict: n_grids > 0 needs grids and grid_of");
+  if (p->n_grids == 0 && (!p->fg.t || !p->fg.XT || !p->fg.t_change || !p->fg.seg))
+    return set_err(ctx, "pf_predict: NULL grid buffer");
+  if (p->fg.T < 1 || p->fg.T > p->fg.T_pad) return set_err(ctx, "pf_predict: bad T / T_pad");
+  if (!p->theta || !p->y_scale || !p->yhat || !p->yhat_lower || !p->yhat_upper)
     return set_err(ctx, "pf_predict: NULL buffer");
   if ((p->trend != nullptr) != (p->trend_lower != nullptr) ||
       (p->trend != nullptr) != (p->trend_upper != nullptr))
@@ -2378,6 +2634,10 @@ int pf_predict(pf_ctx *ctx, const pf_predict_args *p, void *stream) {
   a.add = p->add_terms;
   a.comp = p->comp;
   a.series_id = p->series_id;
+  if (p->n_grids > 0) {
+    a.grids = p->grids;
+    a.grid_of = p->grid_of;
+  }
   a.n_comp = p->comp ? p->n_comp : 0;
   if (a.n_comp < 0 || a.n_comp > PF_MAX_COMP) return set_err(ctx, "pf_predict: n_comp must be in [0, PF_MAX_COMP]");
   for (int b = 0; b < a.n_comp; ++b) {

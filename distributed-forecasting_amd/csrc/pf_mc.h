@@ -452,7 +452,9 @@ __device__ __forceinline__ void mc_rows(const PredKArgs &a, const PredSeries &ps
 }
 
 template <int KMAX>
-__global__ __launch_bounds__(PF_MC_WAVES * 64) void k_predict_mc(PredKArgs a) {
+__global__ __launch_bounds__(PF_MC_WAVES * 64) void k_predict_mc(PredKArgs a0) {
+  PredKArgs a = a0;
+  if (a0.grid_of) bind_pred_grid(a, blockIdx.y);
   constexpr int NT = PF_MC_WAVES * 64;
   constexpr int SPT = (64 * PF_NQ) / NT;  // samples per thread in the setup
   __shared__ PredSeries ps;

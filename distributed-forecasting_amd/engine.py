@@ -201,15 +201,18 @@ def _device_dates(ds_ns: np.ndarray, dev) -> torch.Tensor:
 def build_grid(ds_ns: np.ndarray, seasons, *, start_ns: int, t_scale_ns: int,
                n_changepoints: int = 25, changepoint_range: float = 0.8,
                t_change: torch.Tensor | None = None, device: int = 0,
-               holidays: HolidaySpec | None = None) -> DeviceGrid:
+               holidays: HolidaySpec | None = None, T_pad: int | None = None) -> DeviceGrid:
     """Design grid on the GPU (K1).  With ``t_change=None`` the changepoints are
     placed (fit grid); otherwise they are reused (predict grid).  ``holidays``
     appends its indicator columns after the Fourier blocks (UPSTREAM
-    make_all_seasonality_features order)."""
+    make_all_seasonality_features order).  ``T_pad`` overrides the row stride
+    (the sub-grids of a ragged batch share the largest one)."""
     ctx = Context.get(device)
     ds_ns = np.ascontiguousarray(np.asarray(ds_ns, dtype=np.int64))
     T = int(ds_ns.shape[0])
-    Tp = pad_rows(T)
+    Tp = pad_rows(T) if T_pad is None else int(T_pad)
+    if Tp < T or Tp % 128:
+        raise ValueError(f"T_pad={Tp} must be a multiple of 128 and >= T={T}")
     K = sum(2 * o for _, _, o in seasons)
     n_extra = holidays.n if holidays is not None else 0
     K += n_extra
@@ -247,6 +250,175 @@ def build_grid(ds_ns: np.ndarray, seasons, *, start_ns: int, t_scale_ns: int,
     ctx.check(rc, "pf_build_grid")
     return DeviceGrid(ds_ns, int(start_ns), int(t_scale_ns), list(seasons), T, Tp, K, S, t, XT,
                       tc, seg, cp_first, cp_idx, S_eff, holidays if n_extra else None)
+
+
+def _to_device_async(a: np.ndarray, dev) -> torch.Tensor:
+    """Host array -> device through a pinned staging copy (torch's caching host
+    allocator keeps it until the copy ran): no stream-ordered pageable stall."""
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if dev.type == "cuda":
+        t = t.pin_memory()
+    return t.to(dev, non_blocking=True)
+
+
+class RaggedGrid:
+    """Series with different date grids in one launch (SURVEY §8a row a0 without
+    one bucket per distinct date set).  Sub-grid g shares T_pad, K, S, the
+    seasonality layout and the holiday spec with the others; series s uses
+    ``grids[grid_of[s]]`` (the kernels bind it per workgroup, pf_problem.grids).
+    Duck-types DeviceGrid for the engine: T is the envelope (max rows).
+
+    Two constructions: ``RaggedGrid(list_of_DeviceGrid, grid_of)`` (any grids,
+    e.g. with holiday columns) or ``RaggedGrid.build(...)`` — every sub-grid
+    in three launches (pf_build_grids) into packed [G, ...] buffers."""
+
+    def __init__(self, grids, grid_of: np.ndarray, device: int = 0):
+        g0 = grids[0]
+        for g in grids[1:]:
+            if (g.T_pad, g.K, g.S, tuple(g.seasons)) != (g0.T_pad, g0.K, g0.S, tuple(g0.seasons)) \
+                    or g.holidays != g0.holidays:
+                raise ValueError("ragged sub-grids must share T_pad, K, S, seasonalities and holidays")
+        self._grids = list(grids)
+        self.G = len(grids)
+        self.T_pad, self.K, self.S = g0.T_pad, g0.K, g0.S
+        self.seasons, self.holidays = list(g0.seasons), g0.holidays
+        self.Ts = np.asarray([g.T for g in grids], np.int64)
+        self.T = int(self.Ts.max())
+        self.packed = None
+        self._set_grid_of(grid_of, device)
+        arr = (L.PfGrid * self.G)(*[g.as_pf() for g in grids])
+        self.table = _to_device_async(np.frombuffer(bytes(arr), np.uint8).copy(),
+                                      torch.device("cuda", device))
+
+    def _set_grid_of(self, grid_of, device):
+        gi = np.ascontiguousarray(np.asarray(grid_of, np.int32))
+        if gi.size and (gi.min() < 0 or gi.max() >= self.G):
+            raise ValueError("grid_of index out of range")
+        self.grid_of_host = gi
+        self.grid_of = _to_device_async(gi, torch.device("cuda", device))
+
+    @classmethod
+    def build(cls, ds_list, seasons, starts, scales, grid_of, *, device: int = 0,
+              T_pad: int | None = None, n_changepoints: int = 25,
+              changepoint_range: float = 0.8, t_change: torch.Tensor | None = None) -> "RaggedGrid":
+        """All sub-grids on the device in three launches (pf_build_grids).
+        ``ds_list[g]``: sorted dates of grid g; ``starts`` / ``scales``: its
+        UPSTREAM start / t_scale (ns).  ``t_change`` ([G, S], a fit grid's
+        packed changepoints): build forecast grids on them instead of placing
+        changepoints."""
+        ctx = Context.get(device)
+        dev = torch.device("cuda", device)
+        self = cls.__new__(cls)
+        G = len(ds_list)
+        Ts = np.asarray([len(d) for d in ds_list], np.int64)
+        Tmax = int(Ts.max())
+        Tp = pad_rows(Tmax) if T_pad is None else int(T_pad)
+        if Tp < Tmax or Tp % 128:
+            raise ValueError(f"T_pad={Tp} must be a multiple of 128 and >= {Tmax}")
+        K = sum(2 * o for _, _, o in seasons)
+        if K == 0:
+            raise ValueError("no seasonality columns")
+        if t_change is None:
+            s_eff = {L.num_changepoints(int(T), n_changepoints, changepoint_range) for T in Ts}
+            if len(s_eff) != 1:
+                raise ValueError("ragged sub-grids must place the same number of changepoints")
+            S_eff = s_eff.pop()
+            S = max(S_eff, 1)
+        else:
+            S = S_eff = int(t_change.shape[1])
+        prm = np.zeros((G, 6), np.int64)
+        irregular, off = [], 0
+        for g, d in enumerate(ds_list):
+            d = np.asarray(d, np.int64)
+            T = d.shape[0]
+            step = int(d[1] - d[0]) if T >= 2 else 0
+            regular = step > 0 and int(d[-1] - d[0]) == step * (T - 1) and bool(np.all(np.diff(d) == step))
+            prm[g] = (off, T, int(starts[g]), int(scales[g]), int(d[0]), step if regular else 0)
+            if not regular:
+                irregular.append(d)
+                off += T
+        buf = np.concatenate([prm.ravel()] + irregular) if irregular else prm.ravel()
+        bd = _to_device_async(buf, dev)
+        t = torch.empty((G, Tp), dtype=torch.float64, device=dev)
+        XT = torch.empty((G, K * Tp), dtype=torch.float64, device=dev)
+        if t_change is None:
+            tc = torch.empty((G, S), dtype=torch.float64, device=dev)
+            cp_idx = torch.empty((G, S), dtype=torch.int32, device=dev)
+            ncp = n_changepoints
+        else:
+            assert t_change.dtype == torch.float64 and t_change.shape[0] == G and t_change.is_contiguous()
+            tc, cp_idx, ncp = t_change, None, -1
+        seg = torch.empty((G, Tp), dtype=torch.int32, device=dev)
+        cp_first = torch.empty((G, S), dtype=torch.int32, device=dev)
+        table = torch.empty(G * ctypes.sizeof(L.PfGrid), dtype=torch.uint8, device=dev)
+        sp = (L.PfSeason * max(1, len(seasons)))()
+        for i, (_, period, order) in enumerate(seasons):
+            sp[i].period = float(period)
+            sp[i].order = int(order)
+        rc = ctx.lib.pf_build_grids(ctx.h, G, _ptr(bd), ctypes.c_void_p(bd.data_ptr() + 8 * G * 6),
+                                    Tmax, Tp, sp, len(seasons), ncp, float(changepoint_range),
+                                    _ptr(t), _ptr(XT), _ptr(tc), _ptr(cp_idx), _ptr(seg),
+                                    _ptr(cp_first), S, _ptr(table), _stream(device))
+        ctx.check(rc, "pf_build_grids")
+        self._grids = None
+        self.G, self.T_pad, self.K, self.S, self.T = G, Tp, K, S, Tmax
+        self.seasons, self.holidays = list(seasons), None
+        self.Ts = Ts
+        self.table = table
+        self.packed = dict(ds=[np.asarray(d, np.int64) for d in ds_list],
+                           starts=np.asarray(starts, np.int64), scales=np.asarray(scales, np.int64),
+                           t=t, XT=XT, t_change=tc, cp_idx=cp_idx, seg=seg, cp_first=cp_first,
+                           S_eff=S_eff, params=bd)
+        self.device = device
+        self._set_grid_of(grid_of, device)
+        return self
+
+    @property
+    def grids(self):
+        """Sub-grids as DeviceGrids (views into the packed buffers when built)."""
+        if self._grids is None:
+            p = self.packed
+            self._grids = [
+                DeviceGrid(p["ds"][g], int(p["starts"][g]), int(p["scales"][g]), list(self.seasons),
+                           int(self.Ts[g]), self.T_pad, self.K, self.S, p["t"][g], p["XT"][g],
+                           p["t_change"][g], p["seg"][g], p["cp_first"][g],
+                           p["cp_idx"][g] if p["cp_idx"] is not None else None, p["S_eff"], None)
+                for g in range(self.G)]
+        return self._grids
+
+    @property
+    def n_grids(self) -> int:
+        return self.G
+
+    @property
+    def fourier_orders(self):
+        o = [0, 0, 0]
+        for i, (_, _, order) in enumerate(self.seasons[:3]):
+            o[i] = order
+        return o
+
+    @property
+    def T_of(self) -> np.ndarray:
+        """Rows of each series' own grid."""
+        return self.Ts[self.grid_of_host]
+
+    def as_pf(self) -> L.PfGrid:
+        if self.packed is not None:
+            p = self.packed
+            return L.PfGrid(self.T, self.T_pad, self.K, self.S, p["t"].data_ptr(), p["XT"].data_ptr(),
+                            p["t_change"].data_ptr(), p["seg"].data_ptr(), p["cp_first"].data_ptr())
+        g0 = self._grids[0]
+        return L.PfGrid(self.T, self.T_pad, self.K, self.S, g0.t.data_ptr(), g0.XT.data_ptr(),
+                        g0.t_change.data_ptr(), g0.seg.data_ptr(), g0.cp_first.data_ptr())
+
+    def tensors(self):
+        out = [self.grid_of, self.table]
+        if self.packed is not None:
+            p = self.packed
+            return out + [p["t"], p["XT"], p["t_change"], p["seg"], p["cp_first"], p["params"]]
+        for g in self._grids:
+            out += [g.t, g.XT, g.t_change, g.seg, g.cp_first]
+        return out
 
 
 def component_blocks(grid: DeviceGrid):
@@ -389,7 +561,12 @@ class Engine:
             assert sig_s.dtype == torch.float64 and tuple(sig_s.shape) == (n, grid.K)
             assert tau_s.is_contiguous() and sig_s.is_contiguous()
             pb.tau_series, pb.sigmas_series = tau_s.data_ptr(), sig_s.data_ptr()
-        pb._keep = (sig, s_a, s_m, y_scaled, cap_scaled, priors)
+        pb.n_grids = 0
+        if isinstance(grid, RaggedGrid):
+            pb.n_grids = grid.n_grids
+            pb.grids = grid.table.data_ptr()
+            pb.grid_of = grid.grid_of.data_ptr()
+        pb._keep = (sig, s_a, s_m, y_scaled, cap_scaled, priors, grid)
         return pb
 
     def prepare(self, grid: DeviceGrid, Y: torch.Tensor, cap: torch.Tensor | None = None):
@@ -411,12 +588,16 @@ class Engine:
             assert cap.dtype == torch.float64 and cap.shape == Y.shape and cap.is_contiguous()
             cap_scaled = torch.empty_like(Y)
         pg = grid.as_pf()
-        rc = self.ctx.lib.pf_prepare(self.ctx.h, n, ctypes.byref(pg),
-                                     L.PF_GROWTH[self.config.growth], _ptr(Y),
-                                     _ptr(cap) if cap_scaled is not None else None,
-                                     _ptr(y_scale), _ptr(y_scaled),
-                                     _ptr(cap_scaled) if cap_scaled is not None else None,
-                                     _ptr(theta), _ptr(status), _stream(self.device))
+        ragged = isinstance(grid, RaggedGrid)
+        if ragged:
+            assert grid.grid_of.numel() == n
+        rc = self.ctx.lib.pf_prepare_ragged(
+            self.ctx.h, n, ctypes.byref(pg), grid.n_grids if ragged else 0,
+            _ptr(grid.table) if ragged else None, _ptr(grid.grid_of) if ragged else None,
+            L.PF_GROWTH[self.config.growth], _ptr(Y),
+            _ptr(cap) if cap_scaled is not None else None, _ptr(y_scale), _ptr(y_scaled),
+            _ptr(cap_scaled) if cap_scaled is not None else None,
+            _ptr(theta), _ptr(status), _stream(self.device))
         self.ctx.check(rc, "pf_prepare")
         return y_scale, y_scaled, theta, status, cap_scaled
 
@@ -505,7 +686,8 @@ class Engine:
         cur = torch.cuda.current_stream(fit.theta.device)
         stream.wait_stream(cur)
         g = fit.grid
-        for t in (fit.theta, fit.y_scale, fit.status, g.t, g.XT, g.t_change, g.seg, g.cp_first):
+        gts = g.tensors() if isinstance(g, RaggedGrid) else [g.t, g.XT, g.t_change, g.seg, g.cp_first]
+        for t in [fit.theta, fit.y_scale, fit.status] + gts:
             t.record_stream(stream)
         for v in predict_kw.values():
             if isinstance(v, torch.Tensor) and v.is_cuda:
@@ -515,8 +697,27 @@ class Engine:
             out = self.predict(fit, fg, **predict_kw)
         return fg, out
 
-    def predict_grid(self, fit: FitResult, ds_ns: np.ndarray) -> DeviceGrid:
+    def predict_grid(self, fit: FitResult, ds_ns) -> DeviceGrid:
+        """Forecast grid on the dates ``ds_ns`` (sorted).  For a ragged fit,
+        ``ds_ns`` is a list with the dates of each sub-grid (same order as
+        ``fit.grid.grids``); the result is a RaggedGrid of forecast grids."""
         g = fit.grid
+        if isinstance(g, RaggedGrid):
+            if len(ds_ns) != g.n_grids:
+                raise ValueError("ragged predict_grid needs one date array per sub-grid")
+            Tp = pad_rows(max(len(d) for d in ds_ns))
+            if g.packed is not None:
+                p = g.packed
+                return RaggedGrid.build(ds_ns, g.seasons, p["starts"], p["scales"], g.grid_of_host,
+                                        device=self.device, T_pad=Tp,
+                                        changepoint_range=self.config.changepoint_range,
+                                        t_change=p["t_change"])
+            fgs = [build_grid(d, sg.seasons, start_ns=sg.start_ns, t_scale_ns=sg.t_scale_ns,
+                              changepoint_range=self.config.changepoint_range,
+                              t_change=sg.t_change, device=self.device, holidays=sg.holidays,
+                              T_pad=Tp)
+                   for sg, d in zip(g.grids, ds_ns)]
+            return RaggedGrid(fgs, g.grid_of_host, self.device)
         return build_grid(ds_ns, g.seasons, start_ns=g.start_ns, t_scale_ns=g.t_scale_ns,
                           changepoint_range=self.config.changepoint_range, t_change=g.t_change,
                           device=self.device, holidays=getattr(g, "holidays", None))
@@ -587,6 +788,14 @@ class Engine:
         if series_id is not None:
             assert series_id.numel() == n and series_id.dtype == torch.int32 and series_id.is_cuda
             a.series_id = series_id.data_ptr()
+        a.n_grids = 0
+        if isinstance(fgrid, RaggedGrid):
+            if not isinstance(fit.grid, RaggedGrid) or \
+                    not np.array_equal(fit.grid.grid_of_host, fgrid.grid_of_host):
+                raise ValueError("a ragged forecast grid needs the ragged fit it was built from")
+            a.n_grids = fgrid.n_grids
+            a.grids = fgrid.table.data_ptr()
+            a.grid_of = fgrid.grid_of.data_ptr()
         rc = self.ctx.lib.pf_predict(self.ctx.h, ctypes.byref(a), _stream(self.device))
         self.ctx.check(rc, "pf_predict")
         return out

@@ -90,3 +90,36 @@ def saturating_matrix(n_series: int, ds_ns: np.ndarray, seed: int = 20261015 + 4
     Y = np.maximum(0.0, lvl * seas + rng.normal(0.0, 1.0, (n_series, T)) * 0.05 * C[:, None])
     cap = np.repeat((1.2 * Y.max(axis=1))[:, None], T, axis=1)
     return Y, cap
+
+
+def staggered_frame(n_stores: int = 10, n_items: int = 50, start="2013-01-01",
+                    end="2017-12-31", n_starts: int = 50, max_delay_days: int = 730,
+                    n_ends: int = 1, config_index: int = 1, seed: int = 20261017):
+    """Store-item table with staggered launches: every series is generated on
+    the full daily grid, then keeps the rows from its own launch date
+    (one of ``n_starts`` dates spread over ``max_delay_days``) and, with
+    ``n_ends`` > 1, stops at one of ``n_ends`` end dates in the last 60 days.
+    A real store-item table's shape (new items, delisted items) instead of
+    the Kaggle table's single shared grid (02_training.py:277-282)."""
+    import pandas as pd
+    ds = daily_dates(start, end)
+    n = n_stores * n_items
+    Y = sales_matrix(n, ds, config_index)
+    rng = np.random.Generator(np.random.PCG64(seed))
+    offs = np.linspace(0, max_delay_days, n_starts).astype(np.int64)
+    first = offs[rng.integers(0, n_starts, n)]
+    ends = np.linspace(0, 60 if n_ends > 1 else 0, n_ends).astype(np.int64)
+    last = ds.shape[0] - ends[rng.integers(0, n_ends, n)]
+    stores = np.repeat(np.arange(1, n_stores + 1), n_items)
+    items = np.tile(np.arange(1, n_items + 1), n_stores)
+    parts = []
+    for s in range(n):
+        sl = slice(int(first[s]), int(last[s]))
+        m = sl.stop - sl.start
+        parts.append(pd.DataFrame({
+            "ds": ds[sl].astype("datetime64[ns]"),
+            "store": np.full(m, stores[s], np.int32),
+            "item": np.full(m, items[s], np.int32),
+            "y": Y[s, sl],
+        }))
+    return pd.concat(parts, ignore_index=True)

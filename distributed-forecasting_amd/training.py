@@ -149,13 +149,11 @@ def forecast_store_items(df: pd.DataFrame, keys=("store", "item"), *, periods: i
     y_list = [y_all[r] for r in rows]
     buckets = B.bucket_groups(ds_list, y_list)
     frames, fits = [], []
-    for bk in buckets:
+
+    def emit(bk, fut, host):
+        # one bucket's rows of the output frame (schema of 02_training.py:307)
         bkeys = gkeys[bk.members]
-        fb = B.FittedBatch.fit_dense(eng, bk.fit_ds, bk.Y, history_dates=bk.history_dates,
-                                     series_ids=B.series_id(bkeys))
-        fut = B.future_dates(bk.history_dates, periods, freq, include_history=True)
-        Tf, out = fb.predict(fut, seed=seed, components=False)
-        host = {k: out[k][:, :Tf].cpu().numpy() for k in ("yhat", "yhat_upper", "yhat_lower")}
+        Tf = len(fut)
         n = len(bk.members)
         yin = np.full((n, Tf), np.nan)
         for i, g in enumerate(bk.members):
@@ -167,12 +165,38 @@ def forecast_store_items(df: pd.DataFrame, keys=("store", "item"), *, periods: i
             fr[k] = np.repeat(bkeys[:, j], Tf).astype(np.int32)
         fr["y"] = yin.reshape(-1).astype(np.float32)
         for k in ("yhat", "yhat_upper", "yhat_lower"):
-            fr[k] = host[k].reshape(-1).astype(np.float32)
+            fr[k] = host[k][:, :Tf].reshape(-1).astype(np.float32)
         frames.append(pd.DataFrame(fr))
-        if params_store is not None:
-            params_store.put_batch(fb, bkeys)
-        if return_fits:
-            fits.append((bkeys, fb))
+
+    # buckets with compatible layouts (seasonalities, changepoint count) but
+    # different date grids share one ragged launch
+    for pack in B.ragged_packs(buckets, cfg):
+        if len(pack) == 1:
+            bk = buckets[pack[0]]
+            bkeys = gkeys[bk.members]
+            fb = B.FittedBatch.fit_dense(eng, bk.fit_ds, bk.Y, history_dates=bk.history_dates,
+                                         series_ids=B.series_id(bkeys))
+            fut = B.future_dates(bk.history_dates, periods, freq, include_history=True)
+            Tf, out = fb.predict(fut, seed=seed, components=False)
+            emit(bk, fut, {k: out[k][:, :Tf].cpu().numpy() for k in ("yhat", "yhat_upper", "yhat_lower")})
+            subs = [(bkeys, fb)]
+        else:
+            bks = [buckets[b] for b in pack]
+            pkeys = np.concatenate([gkeys[bk.members] for bk in bks])
+            rb = B.RaggedFittedBatch.fit_buckets(eng, bks, series_ids=B.series_id(pkeys))
+            futs = rb.future(periods, freq)
+            _, out = rb.predict(futs, seed=seed, components=False)
+            host = {k: out[k].cpu().numpy() for k in ("yhat", "yhat_upper", "yhat_lower")}
+            subs = []
+            for j, bk in enumerate(bks):
+                r0, r1 = int(rb.row0[j]), int(rb.row0[j + 1])
+                emit(bk, futs[j], {k: v[r0:r1] for k, v in host.items()})
+                subs.append((pkeys[r0:r1], rb.sub_batch(j)))
+        for bkeys, fb in subs:
+            if params_store is not None:
+                params_store.put_batch(fb, bkeys)
+            if return_fits:
+                fits.append((bkeys, fb))
     cols = ["ds"] + keys + ["y", "yhat", "yhat_upper", "yhat_lower"]
     res = (pd.concat(frames, ignore_index=True) if frames else
            pd.DataFrame({c: pd.Series(dtype=("datetime64[ns]" if c == "ds" else

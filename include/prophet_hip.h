@@ -89,6 +89,17 @@ typedef struct {
    * prior scales, or NULL to use the shared tau / sigmas above.            */
   const double *tau_series;     /* [n_series]      changepoint_prior_scale   */
   const double *sigmas_series;  /* [n_series * K]  per-column prior scales   */
+  /* Ragged batches (series with different date grids in one launch; the
+   * reference's applyInPandas groups each carry their own history,
+   * notebooks/prophet/02_training.py:277-307): grids is a DEVICE array of
+   * n_grids pf_grid descriptors (device pointers inside), grid_of a DEVICE
+   * [n_series] index into it.  Every grid shares T_pad, K, S and the
+   * seasonality layout; `grid` above is then the envelope: T = max T over the
+   * grids, T_pad / K / S the shared values (its pointers are not read).
+   * n_grids = 0: every series uses `grid`.                                  */
+  int32_t n_grids;
+  const pf_grid *grids;
+  const int32_t *grid_of;
 } pf_problem;
 
 typedef struct {
@@ -156,6 +167,24 @@ int pf_build_grid(pf_ctx *ctx, const int64_t *ds_ns, int T, int T_pad,
                   int32_t *seg_out, int32_t *cp_first_out, int S,
                   void *stream);
 
+/* Ragged design builder: n_grids grids (one per distinct history, all with
+ * the same seasonalities, T_pad and S) in three launches, for pf_problem.grids
+ * / pf_predict_args.grids.  DEVICE inputs: grid_params[n_grids*6] int64 =
+ * {offset into ds_ns, T, start_ns, t_scale_ns, first_ns, step_ns} per grid
+ * (step_ns > 0: dates first + i*step generated on the device, ds_ns unread
+ * for that grid; else ds_ns[offset + i]).  T_max = max T (host).  DEVICE
+ * outputs, grid g at: t_out[g*T_pad], XT_out[g*K*T_pad], t_change_io[g*S]
+ * (input when n_changepoints < 0: forecast grids on their fit's
+ * changepoints), cp_idx_out[g*S], seg_out[g*T_pad], cp_first_out[g*S], and
+ * grids_out[g] = the pf_grid descriptor pointing into them.  No extra
+ * (holiday) columns: use pf_build_grid per grid for those.                 */
+int pf_build_grids(pf_ctx *ctx, int n_grids, const int64_t *grid_params, const int64_t *ds_ns,
+                   int T_max, int T_pad, const pf_season *seasons_host, int n_season,
+                   int n_changepoints, double changepoint_range,
+                   double *t_out, double *XT_out, double *t_change_io, int32_t *cp_idx_out,
+                   int32_t *seg_out, int32_t *cp_first_out, int S, pf_grid *grids_out,
+                   void *stream);
+
 /* ------------------------------------------ scaling + Prophet init (a1, a4)
  * y [n_series*T_pad] raw (pad rows ignored) → y_scale[n], y_scaled[n*T_pad],
  * theta0[n*P] (linear_growth_init; delta=beta=0; sigma_obs=1) and
@@ -164,6 +193,15 @@ int pf_prepare(pf_ctx *ctx, int n_series, const pf_grid *grid, int growth,
                const double *y, const double *cap,
                double *y_scale, double *y_scaled, double *cap_scaled,
                double *theta0, int32_t *status, void *stream);
+
+/* pf_prepare for a ragged batch: series s is scaled and initialised on its
+ * own grid grids_dev[grid_of[s]] (DEVICE arrays, see pf_problem.grids);
+ * envelope as in pf_problem.grid.                                          */
+int pf_prepare_ragged(pf_ctx *ctx, int n_series, const pf_grid *envelope, int n_grids,
+                      const pf_grid *grids_dev, const int32_t *grid_of, int growth,
+                      const double *y, const double *cap,
+                      double *y_scale, double *y_scaled, double *cap_scaled,
+                      double *theta0, int32_t *status, void *stream);
 
 /* ------------------------------------------- K2: batched objective + grad
  * f[n] = -log posterior (Stan propto), g[n*P] = its gradient.            */
@@ -227,6 +265,13 @@ typedef struct {
    * (store, item)) so samples do not depend on batch position; NULL: use
    * the batch index.                                                      */
   const uint32_t *series_id;
+  /* ragged forecasts (see pf_problem.grids): DEVICE pf_grid[n_grids] of
+   * forecast grids (each relative to its fit's start / t_scale / t_change)
+   * and DEVICE grid_of[n_series]; fg is the envelope (T = max rows, shared
+   * T_pad / K / S).  Rows past a series' own T are not written.            */
+  int32_t n_grids;
+  const pf_grid *grids;
+  const int32_t *grid_of;
 } pf_predict_args;
 
 int pf_predict(pf_ctx *ctx, const pf_predict_args *args, void *stream);
