@@ -145,3 +145,35 @@ def test_ragged_params_store_round_trip(tmp_path):
     assert len(m) > 0
     d = np.abs(m["yhat"].to_numpy(np.float64) - m["yhat_srv"].to_numpy(np.float64))
     assert np.max(d / np.maximum(1.0, np.abs(m["yhat"].to_numpy(np.float64)))) <= 1e-5
+
+
+def test_ragged_irregular_grids_and_layout_split():
+    """Series with NaN gaps (irregular date grids: dates read from the ds
+    array, not generated) and a 20-day series (15 changepoints: its own pack)
+    through forecast_store_items equal the per-group reference path."""
+    df = synthetic.staggered_frame(1, 8, n_starts=3, n_ends=2, max_delay_days=300)
+    y = df["y"].to_numpy().copy()
+    g1 = np.flatnonzero((df["item"] == 2).to_numpy())
+    y[g1[100:130]] = np.nan                       # a month missing
+    g2 = np.flatnonzero((df["item"] == 5).to_numpy())
+    y[g2[::97]] = np.nan                          # scattered NaNs
+    df["y"] = y
+    short = df[df["item"] == 7].tail(20).assign(item=9)
+    df = pd.concat([df, short], ignore_index=True)
+    gkeys, rows = training.group_frame(df, ["store", "item"])
+    ds_all = B.to_ns(df["ds"])
+    bks = B.bucket_groups([ds_all[r] for r in rows], [y_ for y_ in
+                                                      (df["y"].to_numpy(np.float64)[r] for r in rows)])
+    packs = B.ragged_packs(bks, ProphetConfig.reference())
+    assert len(packs) == 2 and sorted(len(p) for p in packs)[0] == 1
+    res = training.forecast_store_items(df)
+    ref = pd.concat([training.forecast_store_item(g.reset_index(drop=True))
+                     for _, g in df.groupby(["store", "item"], sort=True)], ignore_index=True)
+    key = ["store", "item", "ds"]
+    a = res.sort_values(key).reset_index(drop=True)
+    b = ref.sort_values(key).reset_index(drop=True)
+    assert len(a) == len(b)
+    for c in key:
+        assert np.array_equal(a[c].to_numpy(), b[c].to_numpy()), c
+    ya, yb = a["yhat"].to_numpy(np.float64), b["yhat"].to_numpy(np.float64)
+    assert np.max(np.abs(ya - yb) / np.maximum(1.0, np.abs(yb))) <= 1e-5

@@ -320,3 +320,23 @@ def test_holiday_record_roundtrip():
     rec = B.holiday_record(spec)
     assert B.holiday_from_record(rec) == spec
     assert B.holiday_from_record({}) is None and B.holiday_record(None) == {}
+
+
+def test_ragged_packs_group_by_layout():
+    """Buckets share a ragged launch iff their auto seasonalities and
+    changepoint counts agree (batch.ragged_packs)."""
+    import numpy as np
+    from distributed_forecasting_amd import batch as B, synthetic
+    from distributed_forecasting_amd.engine import ProphetConfig
+    ds = synthetic.daily_dates()
+    y = np.arange(ds.shape[0], dtype=np.float64)
+    parts = [(ds[s:], y[s:]) for s in (0, 30, 365)]          # >= 730 days: yearly on
+    parts += [(ds[-400:], y[-400:]), (ds[-300:], y[-300:])]  # < 730 days: no yearly
+    parts += [(ds[-20:], y[-20:])]                           # 20 rows: 15 changepoints
+    bks = B.bucket_groups([p[0] for p in parts], [p[1] for p in parts])
+    packs = B.ragged_packs(bks, ProphetConfig())              # auto seasonalities
+    assert sorted(len(p) for p in packs) == [1, 2, 3], packs
+    # the reference config forces yearly + weekly on: only the changepoint
+    # count splits
+    packs = B.ragged_packs(bks, ProphetConfig.reference())
+    assert sorted(len(p) for p in packs) == [1, 5], packs

@@ -1,11 +1,15 @@
 """CPU: the oracle against the known-answer tests of SURVEY.md §8c and the
 committed golden fixtures (tests/golden/make_golden.py)."""
+import os
+
 import numpy as np
 import pytest
 
 from distributed_forecasting_amd import synthetic
 from oracle import prophet_oracle as po
 from oracle import stan_oracle as so
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 NSD = po.NS_PER_DAY
 
@@ -181,3 +185,18 @@ def test_rolling_median_by_h_small():
     assert hs.tolist() == [1, 2, 3] and v.tolist() == [2.0, 4.0, 8.0]
     hs, v = po.rolling_median_by_h(x, h, 3)
     assert hs.tolist() == [2, 3] and v.tolist() == [3.0, 7.0]
+
+
+def test_oracle_sanitizers():
+    """The C oracle under AddressSanitizer + UndefinedBehaviorSanitizer
+    (host only): objective, Stan L-BFGS, Hessians and the damped polish for
+    linear, logistic and flat growth (oracle/asan_check.c)."""
+    import shutil
+    import subprocess
+    if shutil.which("make") is None or shutil.which("cc") is None:
+        pytest.skip("no host toolchain")
+    r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "asan"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr
+    assert r.stdout.count("cert 1") == 3, r.stdout
