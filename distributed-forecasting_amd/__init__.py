@@ -21,6 +21,7 @@ from .diagnostics import cv_metrics_batch, cv_metrics_device, generate_cutoffs  
 from .engine import future_dates  # noqa: F401
 from .holidays import HolidaySpec, holiday_spec  # noqa: F401
 from . import tuning  # noqa: F401
+from .graphs import ForecastStep  # noqa: F401
 from . import serialize  # noqa: F401
 from .tuning import hyperparameter_search, sample_trials  # noqa: F401
 
@@ -32,4 +33,4 @@ __all__ = ["Engine", "ProphetConfig", "FitResult", "DeviceGrid", "build_grid", "
            "ParamsStore", "ForecastStoreItemModel", "predict_udf", "register_model",
            "cv_metrics_batch", "cv_metrics_device", "generate_cutoffs", "allocate_forecasts",
            "forecast_partitions", "HolidaySpec", "holiday_spec", "tuning",
-           "hyperparameter_search", "sample_trials"]
+           "hyperparameter_search", "sample_trials", "ForecastStep"]

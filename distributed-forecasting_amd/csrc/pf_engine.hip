@@ -2088,7 +2088,7 @@ void pf_default_fit_opts(pf_fit_opts *o) {
   o->polish = 1;
   o->polish_max_iter = 50;  // accepted Newton steps (damped logistic fits from far away need ~30)
   o->lbfgs_warmup = 60;
-  o->lbfgs_warmup_evals = 0;
+  o->lbfgs_warmup_evals = 90;  // also end a warm-up pass at 90 evaluations (tools/diag_warmup.py)
   o->tile_min_series = 2048;
 }
 

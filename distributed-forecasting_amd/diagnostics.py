@@ -123,7 +123,8 @@ def insample_metrics(engine: E.Engine, y: torch.Tensor, yhat: torch.Tensor,
     ff = yhat[:, :T].contiguous()
     lo = yhat_lower[:, :T].contiguous() if yhat_lower is not None else None
     hi = yhat_upper[:, :T].contiguous() if yhat_upper is not None else None
-    gs = torch.tensor([0, T], dtype=torch.int32, device=dev)
+    # built on the device (no host copy: capturable into a hipGraph)
+    gs = torch.arange(2, dtype=torch.int32, device=dev) * T
     met = torch.empty((n, len(L.CV_METRICS)), dtype=torch.float64, device=dev)
     a = L.PfCvArgs(n, T, 1, T, gs.data_ptr(), yy.data_ptr(), ff.data_ptr(),
                    lo.data_ptr() if lo is not None else None,

@@ -1,0 +1,101 @@
+"""Captured hipGraphs of the fit + forecast step.
+
+A batch of series on one date grid runs ~15 kernels per step (K1 grids,
+prepare, the fused fit, forecast grid, K4/K5, K6) whose host side — ctypes
+argument structs, torch allocations, Python — costs about as much as the
+small launches themselves.  For a serving / training loop that sees batches
+of one shape (the reference's nightly refit of every (store, item) on the
+same calendar, 02_training.py:305-307), ``ForecastStep`` records the step's
+launches once into a hipGraph and replays it: every kernel still runs on
+every replay over whatever is in the static input buffer ``Y`` (refresh it
+with ``set_inputs``); only the host-side launch work is recorded.
+
+Capture needs the engine's context workspace to be allocated already (no
+hipMalloc while capturing): the constructor runs the step once eagerly
+first.  RCCL collectives stay outside the graph (run them after replay).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import engine as E
+from . import diagnostics
+
+
+class ForecastStep:
+    """One fit + forecast (+ in-sample metrics) step for a fixed batch shape:
+    ``n`` series on the sorted history dates ``ds_ns``, ``horizon`` future
+    periods of ``freq_ns``.  ``run()`` launches eagerly; ``replay()`` replays
+    the captured graph (``capture()`` first).  Outputs (device tensors, valid
+    columns [:Tf]) are in ``out`` after either."""
+
+    def __init__(self, engine: E.Engine, ds_ns: np.ndarray, n: int, *, horizon: int = 90,
+                 freq_ns: int = E.NS_PER_DAY, series_id: torch.Tensor | None = None,
+                 seed: int = 0, metrics: bool = True, interval_method: str | None = None,
+                 components: bool = False):
+        self.engine = engine
+        cfg = engine.config
+        self.ds = np.asarray(ds_ns, np.int64)
+        self.T = int(self.ds.shape[0])
+        self.seasons = cfg.seasons(int(self.ds[0]), int(self.ds[-1]),
+                                   int(np.min(np.diff(self.ds))) if self.T > 1 else 0)
+        self.fut = E.future_dates(self.ds, horizon, freq_ns)
+        self.Tf = int(self.fut.shape[0])
+        dev = torch.device("cuda", engine.device)
+        self.Y = torch.zeros((n, E.pad_rows(self.T)), dtype=torch.float64, device=dev)
+        self.series_id = series_id
+        self.seed = seed
+        self.metrics = metrics
+        self.interval_method = interval_method
+        self.components = components
+        self.graph = None
+        self.out = None
+
+    def set_inputs(self, Y) -> None:
+        """Copy a new batch ([n, T] raw y, host or device) into the static buffer."""
+        src = Y if isinstance(Y, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(Y))
+        self.Y[:, :self.T].copy_(src, non_blocking=True)
+
+    def _step(self) -> dict:
+        eng = self.engine
+        grid = E.build_grid(self.ds, self.seasons, start_ns=int(self.ds[0]),
+                            t_scale_ns=int(self.ds[-1] - self.ds[0]),
+                            n_changepoints=eng.config.n_changepoints,
+                            changepoint_range=eng.config.changepoint_range, device=eng.device)
+        fit = eng.fit(grid, self.Y)
+        fg = eng.predict_grid(fit, self.fut)
+        out = eng.predict(fit, fg, seed=self.seed, components=self.components,
+                          series_id=self.series_id, interval_method=self.interval_method)
+        res = {"fit": fit, "forecast": out, "grid": grid, "forecast_grid": fg}
+        if self.metrics:
+            res["metrics"] = diagnostics.insample_metrics(
+                eng, self.Y[:, :self.T], out["yhat"], out["yhat_lower"], out["yhat_upper"])
+        return res
+
+    def run(self) -> dict:
+        """Eager launches (also the warm-up before ``capture``)."""
+        self.out = self._step()
+        return self.out
+
+    def capture(self) -> "ForecastStep":
+        """Record the step into a hipGraph (runs it eagerly once first, on a
+        side stream as torch's capture protocol asks)."""
+        cur = torch.cuda.current_stream(self.Y.device)
+        side = torch.cuda.Stream(self.Y.device)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            self._step()
+        cur.wait_stream(side)
+        torch.cuda.synchronize(self.Y.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.out = self._step()
+        self.graph = g
+        return self
+
+    def replay(self) -> dict:
+        if self.graph is None:
+            raise RuntimeError("capture() first")
+        self.graph.replay()
+        return self.out
