@@ -25,6 +25,7 @@ EXPORTED = ["pf_ctx_create", "pf_ctx_destroy", "pf_last_error", "pf_default_fit_
             "pf_hessian", "pf_prepare_ragged", "pf_build_grids"]
 PF_MAX_COMP = 32  # include/prophet_hip.h
 PF_INTERVAL = {"exact": 0, "sample": 1}
+PF_PREDICT_DET, PF_PREDICT_MC = 1, 2
 CV_METRICS = ["mse", "rmse", "mae", "mape", "smape", "coverage", "mdape"]
 
 
@@ -72,7 +73,7 @@ class PfPredictArgs(ctypes.Structure):
                 ("mult_terms", vp), ("add_terms", vp),
                 ("n_comp", i32), ("comp_col0", i32 * PF_MAX_COMP), ("comp_ncol", i32 * PF_MAX_COMP), ("comp", vp),
                 ("series_id", vp),
-                ("n_grids", i32), ("grids", vp), ("grid_of", vp)]
+                ("n_grids", i32), ("grids", vp), ("grid_of", vp), ("parts", i32)]
 
 
 class PfCvArgs(ctypes.Structure):

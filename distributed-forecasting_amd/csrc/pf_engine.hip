@@ -1835,6 +1835,7 @@ struct PredKArgs {
   const double *cap;          // [n][Tp] logistic capacity / y_scale on the predicted rows
   float zthr;                 // deterministic-trend rows: tail threshold on the standard
                               // normal draws (0: always the general selection)
+  int row_thr;                // random rows: selection thresholds carried row to row (0: off)
   const pf_grid *grids;       // ragged forecasts: series s predicts on grids[grid_of[s]]
   const int32_t *grid_of;     // (NULL: every series on t / XT / seg above)
 };
@@ -1918,31 +1919,38 @@ __device__ __forceinline__ double pred_trend(const PredKArgs &a, const PredSerie
   return ps.mseg[0];
 }
 
+// x . (beta s_m) and x . (beta s_a) over the K features of one row, in
+// feature order; the loads are issued 16 at a time (one memory latency per
+// 16 features instead of one per feature)
+__device__ __forceinline__ void pred_row_dot(const PredKArgs &a, const PredSeries &ps, int row,
+                                             double &xbm, double &xba) {
+  constexpr int CH = 16;
+  const int K = a.K;
+  for (int f0 = 0; f0 < K; f0 += CH) {
+    double xv[CH];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) xv[j] = (f0 + j < K) ? a.XT[(size_t)(f0 + j) * a.Tp + row] : 0.0;
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      if (f0 + j < K) {
+        xbm += xv[j] * ps.bm[f0 + j];
+        xba += xv[j] * ps.ba[f0 + j];
+      }
+    }
+  }
+}
+
 // ---- K4: point forecast + components + deterministic-row intervals.
 // Grid (ceil(Tf/256), n_series), thread per row.  Under PF_INTERVAL_EXACT
 // the interval endpoints of deterministic rows are exact order-statistic
 // draws (pf_ostat.h); rows left to k_predict_mc are not written here.
-template <int KMAX>
-__global__ __launch_bounds__(256) void k_predict_det(PredKArgs a0) {
-  __shared__ PredSeries ps;
-  const int series = blockIdx.y;
-  PredKArgs a = a0;
-  if (a0.grid_of) bind_pred_grid(a, series);
-  const uint32_t sid = a.series_id ? a.series_id[series] : (uint32_t)series;
-  pred_setup(a, series, ps);
-  __syncthreads();
-  const int row = blockIdx.x * 256 + threadIdx.x;
-  if (row >= a.Tf) return;
-  const double t_max = a.t[a.Tf - 1];
+__device__ __forceinline__ void det_row(const PredKArgs &a, const PredSeries &ps, int series,
+                                        uint32_t sid, int row, double t_max) {
   const double ysc = ps.ysc;
   const double ti = a.t[row];
   const int sg = a.seg[row];
   double xbm = 0.0, xba = 0.0;
-  for (int f = 0; f < a.K; ++f) {
-    const double xv = a.XT[(size_t)f * a.Tp + row];
-    xbm += xv * ps.bm[f];
-    xba += xv * ps.ba[f];
-  }
+  pred_row_dot(a, ps, row, xbm, xba);
   if (a.comp) {
     // component blocks: contiguous column ranges (UPSTREAM
     // predict_seasonal_components, MAP: the mean); additive parts x y_scale
@@ -1986,7 +1994,26 @@ __global__ __launch_bounds__(256) void k_predict_det(PredKArgs a0) {
   }
   a.ylo[o] = ylo;
   a.yhi[o] = yhi;
-  if (a.tr) { a.trlo[o] = (float)trend; a.trhi[o] = (float)trend; }
+  if (a.tr) { a.trlo[o] = (float)trend; a.trhi[o] = (float)trend; }}
+
+// PF_DET_RPT rows per thread (strided by the block): the per-series setup is
+// paid once per 256 * PF_DET_RPT rows
+#define PF_DET_RPT 4
+template <int KMAX>
+__global__ __launch_bounds__(256) void k_predict_det(PredKArgs a0) {
+  __shared__ PredSeries ps;
+  const int series = blockIdx.y;
+  PredKArgs a = a0;
+  if (a0.grid_of) bind_pred_grid(a, series);
+  const uint32_t sid = a.series_id ? a.series_id[series] : (uint32_t)series;
+  pred_setup(a, series, ps);
+  __syncthreads();
+  const double t_max = a.t[a.Tf - 1];
+#pragma unroll 1
+  for (int r = 0; r < PF_DET_RPT; ++r) {
+    const int row = (blockIdx.x * PF_DET_RPT + r) * 256 + threadIdx.x;
+    if (row < a.Tf) det_row(a, ps, series, sid, row, t_max);
+  }
 }
 
 #include "pf_mc.h"
@@ -2680,16 +2707,21 @@ int pf_predict(pf_ctx *ctx, const pf_predict_args *p, void *stream) {
     }
   }
   a.method = p->interval_method;
+  a.row_thr = !getenv_flag("PF_MC_GENERAL_SELECT");
   a.cap = p->cap_scaled;
   if (a.growth == PF_GROWTH_LOGISTIC && !a.cap)
     return set_err(ctx, "pf_predict: logistic growth needs cap_scaled on the predicted rows");
   if (a.method != PF_INTERVAL_EXACT && a.method != PF_INTERVAL_SAMPLE)
     return set_err(ctx, "pf_predict: interval_method must be PF_INTERVAL_EXACT or PF_INTERVAL_SAMPLE");
-  const dim3 grid((a.Tf + 255) / 256, a.n_series);
-  PF_TIMED_LAUNCH(ctx, "k_predict_det", grid.x * grid.y, (hipStream_t)stream,
-                  (k_predict_det<64>), grid, dim3(256), 0, (hipStream_t)stream, a);
-  PF_HIP(ctx, hipGetLastError());
-  if (a.N > 0) {
+  const int parts = p->parts == 0 ? (PF_PREDICT_DET | PF_PREDICT_MC) : p->parts;
+  if (parts & ~(PF_PREDICT_DET | PF_PREDICT_MC)) return set_err(ctx, "pf_predict: bad parts");
+  const dim3 grid((a.Tf + 256 * PF_DET_RPT - 1) / (256 * PF_DET_RPT), a.n_series);
+  if (parts & PF_PREDICT_DET) {
+    PF_TIMED_LAUNCH(ctx, "k_predict_det", grid.x * grid.y, (hipStream_t)stream,
+                    (k_predict_det<64>), grid, dim3(256), 0, (hipStream_t)stream, a);
+    PF_HIP(ctx, hipGetLastError());
+  }
+  if (a.N > 0 && (parts & PF_PREDICT_MC)) {
     // exact mode: one block (PF_MC_WAVES waves) per series over the random
     // rows (the horizon); sample mode: every row, <= 64 rows per wave
     // sample mode: every row; a block per (series, row range) while the

@@ -726,11 +726,16 @@ class Engine:
                 seed: int = 0, components: bool = True,
                 series_id: torch.Tensor | None = None,
                 interval_method: str | None = None,
-                cap: torch.Tensor | None = None) -> dict:
+                cap: torch.Tensor | None = None,
+                mc_stream: torch.cuda.Stream | None = None) -> dict:
         """Point forecast + MC intervals for every fitted series on ``fgrid``.
         Returns float32 device tensors [n, fgrid.T_pad] (valid columns :T).
         ``series_id`` (int32/uint32 [n] on the device) keys each series' RNG
-        stream so the intervals do not depend on the batch composition."""
+        stream so the intervals do not depend on the batch composition.
+        ``mc_stream``: launch the Monte-Carlo rows (K5) there, concurrently
+        with K4 on the current stream (both only read theta and write disjoint
+        rows); the caller joins (``current.wait_stream(mc_stream)``) before
+        reading the future rows' intervals."""
         n = fit.theta.shape[0]
         dev = fit.theta.device
         if fit.theta.shape[1] != 3 + fgrid.S + fgrid.K:
@@ -796,6 +801,21 @@ class Engine:
             a.n_grids = fgrid.n_grids
             a.grids = fgrid.table.data_ptr()
             a.grid_of = fgrid.grid_of.data_ptr()
+        if mc_stream is None:
+            a.parts = 0
+            rc = self.ctx.lib.pf_predict(self.ctx.h, ctypes.byref(a), _stream(self.device))
+            self.ctx.check(rc, "pf_predict")
+            return out
+        cur = torch.cuda.current_stream(dev)
+        mc_stream.wait_stream(cur)
+        a.parts = L.PF_PREDICT_MC
+        rc = self.ctx.lib.pf_predict(self.ctx.h, ctypes.byref(a), ctypes.c_void_p(mc_stream.cuda_stream))
+        self.ctx.check(rc, "pf_predict (mc part)")
+        if not torch.cuda.is_current_stream_capturing():
+            # (a captured graph's pool keeps its blocks for the graph's life)
+            for v in list(out.values()) + [fit.theta, fit.y_scale]:
+                v.record_stream(mc_stream)
+        a.parts = L.PF_PREDICT_DET
         rc = self.ctx.lib.pf_predict(self.ctx.h, ctypes.byref(a), _stream(self.device))
-        self.ctx.check(rc, "pf_predict")
+        self.ctx.check(rc, "pf_predict (det part)")
         return out

@@ -51,6 +51,8 @@ class ForecastStep:
         self.components = components
         self.graph = None
         self.out = None
+        # K5 (Monte-Carlo rows) on a side stream, concurrent with K4 and K6
+        self.mc_stream = torch.cuda.Stream(dev)
 
     def set_inputs(self, Y) -> None:
         """Copy a new batch ([n, T] raw y, host or device) into the static buffer."""
@@ -63,14 +65,29 @@ class ForecastStep:
                             t_scale_ns=int(self.ds[-1] - self.ds[0]),
                             n_changepoints=eng.config.n_changepoints,
                             changepoint_range=eng.config.changepoint_range, device=eng.device)
+        # the forecast grid needs only the fit grid's changepoints: build it
+        # on the side stream while the fit runs
+        cur = torch.cuda.current_stream(self.Y.device)
+        self.mc_stream.wait_stream(cur)
+        with torch.cuda.stream(self.mc_stream):
+            fg = E.build_grid(self.fut, self.seasons, start_ns=grid.start_ns,
+                              t_scale_ns=grid.t_scale_ns,
+                              changepoint_range=eng.config.changepoint_range,
+                              t_change=grid.t_change, device=eng.device)
         fit = eng.fit(grid, self.Y)
-        fg = eng.predict_grid(fit, self.fut)
+        cur.wait_stream(self.mc_stream)
         out = eng.predict(fit, fg, seed=self.seed, components=self.components,
-                          series_id=self.series_id, interval_method=self.interval_method)
+                          series_id=self.series_id, interval_method=self.interval_method,
+                          mc_stream=self.mc_stream)
         res = {"fit": fit, "forecast": out, "grid": grid, "forecast_grid": fg}
+        method = self.interval_method or eng.config.interval_method
+        if method == "sample":
+            cur.wait_stream(self.mc_stream)     # K5 writes the history rows' intervals too
         if self.metrics:
+            # exact intervals: the history rows are written by K4 on this stream
             res["metrics"] = diagnostics.insample_metrics(
                 eng, self.Y[:, :self.T], out["yhat"], out["yhat_lower"], out["yhat_upper"])
+        cur.wait_stream(self.mc_stream)
         return res
 
     def run(self) -> dict:

@@ -48,3 +48,26 @@ def test_graph_replay_equals_eager():
             assert torch.equal(e[k][:, :Tf], r[k][:, :Tf]), k
     assert not torch.equal(r1["theta"], r2["theta"])
     assert bool((r2["status"] == 70).all())
+
+
+@pytest.mark.parametrize("method", ["exact", "sample"])
+def test_predict_parts_on_two_streams_equal_one_call(method):
+    """pf_predict_args.parts: K4 on the current stream and K5 on a side
+    stream give the same outputs as one call."""
+    ds = synthetic.daily_dates("2015-01-01", "2017-12-31")
+    n = 24
+    Y = synthetic.sales_matrix(n, ds)
+    eng = dfa.Engine(0)
+    seasons = eng.config.seasons(int(ds[0]), int(ds[-1]), int(ds[1] - ds[0]))
+    g = dfa.build_grid(ds, seasons, start_ns=int(ds[0]), t_scale_ns=int(ds[-1] - ds[0]))
+    Yd = torch.zeros((n, g.T_pad), dtype=torch.float64, device="cuda")
+    Yd[:, :g.T] = torch.from_numpy(Y).cuda()
+    fit = eng.fit(g, Yd)
+    fg = eng.predict_grid(fit, dfa.future_dates(ds, 90))
+    one = eng.predict(fit, fg, seed=5, interval_method=method)
+    side = torch.cuda.Stream()
+    two = eng.predict(fit, fg, seed=5, interval_method=method, mc_stream=side)
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    for k in one:
+        assert torch.equal(one[k][:, :fg.T], two[k][:, :fg.T]), k
