@@ -1835,7 +1835,6 @@ struct PredKArgs {
   const double *cap;          // [n][Tp] logistic capacity / y_scale on the predicted rows
   float zthr;                 // deterministic-trend rows: tail threshold on the standard
                               // normal draws (0: always the general selection)
-  int row_thr;                // random rows: selection thresholds carried row to row (0: off)
   const pf_grid *grids;       // ragged forecasts: series s predicts on grids[grid_of[s]]
   const int32_t *grid_of;     // (NULL: every series on t / XT / seg above)
 };
@@ -2707,7 +2706,6 @@ int pf_predict(pf_ctx *ctx, const pf_predict_args *p, void *stream) {
     }
   }
   a.method = p->interval_method;
-  a.row_thr = !getenv_flag("PF_MC_GENERAL_SELECT");
   a.cap = p->cap_scaled;
   if (a.growth == PF_GROWTH_LOGISTIC && !a.cap)
     return set_err(ctx, "pf_predict: logistic growth needs cap_scaled on the predicted rows");

@@ -68,25 +68,10 @@ __device__ __forceinline__ void wave_sort_asc_n(float (&x)[NS]) {
 // ties — trend samples without a new changepoint all equal the point trend).
 // Falls back to a bisection on the ordered bit patterns when kk + 2 > 64 or
 // more than 64 keys fall below U_s.  buf: NS * 64 floats of wave-private LDS.
-// inclusive prefix sum of an int across the wave
-__device__ __forceinline__ int wave_prefix_i32(int v) {
-  v += dpp_i32<PF_DPP_SHR(1)>(v);
-  v += dpp_i32<PF_DPP_SHR(2)>(v);
-  v += dpp_i32<PF_DPP_SHR(4)>(v);
-  v += dpp_i32<PF_DPP_SHR(8)>(v);
-  v += dpp_i32<PF_DPP_BCAST15, 0xA>(v);
-  v += dpp_i32<PF_DPP_BCAST31, 0xC>(v);
-  return v;
-}
-
-// Rank of the next row's threshold (PF_MC_THR_RANK past kk): the keys below
-// a threshold at that rank of the previous row number ~kk + 16 (binomial
-// spread ~6), inside [kk + 2, 64] for almost every row.
-#define PF_MC_THR_RANK 16
 template <int NS>
 __device__ __forceinline__ void wave_tail_select(const float (&v)[PF_NQ], const float (&tv)[PF_NQ],
                                                  const int (&kk)[NS], float *buf, float (&o0)[NS],
-                                                 float (&o1)[NS], float (&thr_next)[NS]) {
+                                                 float (&o1)[NS]) {
   const int lane = pf_lane();
   auto src = [&](int s, int q) -> float { return (s < 2) ? v[q] : tv[q]; };
   float lm[NS];
@@ -135,9 +120,6 @@ __device__ __forceinline__ void wave_tail_select(const float (&v)[PF_NQ], const 
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     const int k = kk[s];
-    const int kt = k + PF_MC_THR_RANK;
-    const float tk = (kt < 64 && kt < M[s] && M[s] <= 64) ? readlane_f32(c[s], kt) : __builtin_nanf("");
-    thr_next[s] = tk;  // key space (negated samples for the upper tails)
     if (k + 1 < 64 && M[s] <= 64) {
       o0[s] = (k < M[s]) ? readlane_f32(c[s], k) : U[s];
       o1[s] = (k + 1 < M[s]) ? readlane_f32(c[s], k + 1) : U[s];
@@ -161,69 +143,16 @@ __device__ __forceinline__ void wave_tail_select(const float (&v)[PF_NQ], const 
   }
 }
 
-// Random-trend rows: the same ranks from the keys strictly below a threshold
-// carried over from the previous row (thr[s], a key value of that row at rank
-// kk + PF_MC_THR_RANK; NaN = none).  Exact whenever every set has between
-// kk + 2 and 64 keys below its threshold (then ranks kk, kk + 1 are among
-// them); returns false otherwise and the caller runs the general
-// wave_tail_select.  On success thr is moved to this row's rank-(kk + 16) key
-// (kept when fewer keys fell below).
-template <int NS>
-__device__ __forceinline__ bool wave_tail_select_thr(const float (&v)[PF_NQ], const float (&tv)[PF_NQ],
-                                                     const int (&kk)[NS], float (&thr)[NS], float *buf,
-                                                     float (&o0)[NS], float (&o1)[NS]) {
-  const int lane = pf_lane();
-  auto src = [&](int s, int q) -> float { return (s < 2) ? v[q] : tv[q]; };
-  int cnt[NS];
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    if (!(thr[s] == thr[s]) || kk[s] + 1 >= 64) return false;  // uniform
-    cnt[s] = 0;
-  }
-#pragma unroll
-  for (int q = 0; q < PF_NQ; ++q) {
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const float x = src(s, q);
-      cnt[s] += ((s & 1) ? (x > -thr[s]) : (x < thr[s])) ? 1 : 0;
-    }
-  }
-  int pre[NS], M[NS];
-  bool ok = true;
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    pre[s] = wave_prefix_i32(cnt[s]);
-    M[s] = __builtin_amdgcn_readlane(pre[s], 63);
-    ok = ok && M[s] >= kk[s] + 2 && M[s] <= 64;
-  }
-  if (!ok) return false;
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    int w = s * 64 + pre[s] - cnt[s];
-#pragma unroll
-    for (int q = 0; q < PF_NQ; ++q) {
-      const float x = src(s, q);
-      if ((s & 1) ? (x > -thr[s]) : (x < thr[s])) buf[w++] = (s & 1) ? -x : x;
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  float c[NS];
-#pragma unroll
-  for (int s = 0; s < NS; ++s) c[s] = (lane < M[s]) ? buf[s * 64 + lane] : INFINITY;
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  wave_sort_asc_n(c);
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const int k = kk[s], kt = k + PF_MC_THR_RANK;
-    o0[s] = readlane_f32(c[s], k);
-    o1[s] = readlane_f32(c[s], k + 1);
-    if (kt < M[s]) thr[s] = readlane_f32(c[s], kt);  // key space
-  }
-  return true;
+// inclusive prefix sum of an int across the wave
+__device__ __forceinline__ int wave_prefix_i32(int v) {
+  v += dpp_i32<PF_DPP_SHR(1)>(v);
+  v += dpp_i32<PF_DPP_SHR(2)>(v);
+  v += dpp_i32<PF_DPP_SHR(4)>(v);
+  v += dpp_i32<PF_DPP_SHR(8)>(v);
+  v += dpp_i32<PF_DPP_BCAST15, 0xA>(v);
+  v += dpp_i32<PF_DPP_BCAST31, 0xC>(v);
+  return v;
 }
-
 
 // Deterministic-trend rows: the samples are yhat + sd z with z standard
 // normal, a monotone map, so the order statistics are those of z.  Ranks
@@ -363,8 +292,6 @@ __device__ __forceinline__ void mc_rows(const PredKArgs &a, const PredSeries &ps
   }
   const int kk4[4] = {a.k_lo, a.k_hi_neg, a.k_lo, a.k_hi_neg};
   const int kk2[2] = {a.k_lo, a.k_hi_neg};
-  // random rows: selection thresholds carried from row to row (NaN: none yet)
-  float thr4[4] = {__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
   for (int c0 = row_b; c0 < row_e; c0 += 64) {
     const int nr = min(64, row_e - c0);
     // lane-per-row deterministic part (same arithmetic as k_predict_det)
@@ -495,16 +422,15 @@ __device__ __forceinline__ void mc_rows(const PredKArgs &a, const PredSeries &ps
         yhi = np_lerp(fmaf(sd, -zo1[1], yh), fmaf(sd, -zo0[1], yh), a.fr_hi);
       } else if (random) {
         float o0[4], o1[4];
-        if (!a.row_thr || !wave_tail_select_thr<4>(v, tv, kk4, thr4, buf, o0, o1))
-          wave_tail_select<4>(v, tv, kk4, buf, o0, o1, thr4);
+        wave_tail_select<4>(v, tv, kk4, buf, o0, o1);
         if (N == 1) { for (int s = 0; s < 4; ++s) o1[s] = o0[s]; }
         ylo = np_lerp(o0[0], o1[0], a.fr_lo);
         yhi = np_lerp(-o1[1], -o0[1], a.fr_hi);
         tlo = np_lerp(o0[2], o1[2], a.fr_lo);
         thi = np_lerp(-o1[3], -o0[3], a.fr_hi);
       } else {
-        float o0[2], o1[2], tn2[2];
-        wave_tail_select<2>(v, v, kk2, buf, o0, o1, tn2);
+        float o0[2], o1[2];
+        wave_tail_select<2>(v, v, kk2, buf, o0, o1);
         if (N == 1) { o1[0] = o0[0]; o1[1] = o0[1]; }
         ylo = np_lerp(o0[0], o1[0], a.fr_lo);
         yhi = np_lerp(-o1[1], -o0[1], a.fr_hi);

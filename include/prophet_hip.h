@@ -272,7 +272,14 @@ typedef struct {
   int32_t n_grids;
   const pf_grid *grids;
   const int32_t *grid_of;
+  /* which kernels to launch: 0 = all; PF_PREDICT_DET = the point forecast,
+   * components and deterministic-row intervals (K4); PF_PREDICT_MC = the
+   * Monte-Carlo rows (K5).  The two parts write disjoint rows and depend only
+   * on theta, so a caller may run them on two streams (join before reading
+   * the intervals).                                                        */
+  int32_t parts;
 } pf_predict_args;
+enum { PF_PREDICT_DET = 1, PF_PREDICT_MC = 2 };
 
 int pf_predict(pf_ctx *ctx, const pf_predict_args *args, void *stream);
 

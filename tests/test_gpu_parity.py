@@ -186,9 +186,7 @@ def test_sample_mode_threshold_selection_is_exact(eng, golden_ref, monkeypatch, 
     general wave selection when a tail holds too few or too many keys): the
     same order statistics, so the sample-mode output is bitwise that of the
     general selection (PF_MC_GENERAL_SELECT=1) on every row, history and
-    horizon.  Random-trend (horizon) rows likewise select from the keys below
-    a threshold carried over from the previous row (pf_mc.h
-    wave_tail_select_thr), also switched off by PF_MC_GENERAL_SELECT."""
+    horizon."""
     ds, Y, fut = golden_ref["ds_ns"], golden_ref["Y"], golden_ref["fut_ns"]
     g = _grid(eng, ds)
     fit = eng.fit(g, _Y(g, Y))
