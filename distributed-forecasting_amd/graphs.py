@@ -106,7 +106,9 @@ class ForecastStep:
         cur.wait_stream(side)
         torch.cuda.synchronize(self.Y.device)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        # thread-local capture: other threads' runtime calls (e.g. the process
+        # group's watchdog querying events) do not invalidate the capture
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             self.out = self._step()
         self.graph = g
         return self
