@@ -420,7 +420,7 @@ __device__ __forceinline__ void mc_rows(const PredKArgs &a, const PredSeries &ps
         // order statistics of yhat + sd z: the same monotone map of z's
         ylo = np_lerp(fmaf(sd, zo0[0], yh), fmaf(sd, zo1[0], yh), a.fr_lo);
         yhi = np_lerp(fmaf(sd, -zo1[1], yh), fmaf(sd, -zo0[1], yh), a.fr_hi);
-      } else if (random) {
+      } else if (random && a.tr) {
         float o0[4], o1[4];
         wave_tail_select<4>(v, tv, kk4, buf, o0, o1);
         if (N == 1) { for (int s = 0; s < 4; ++s) o1[s] = o0[s]; }
@@ -429,6 +429,7 @@ __device__ __forceinline__ void mc_rows(const PredKArgs &a, const PredSeries &ps
         tlo = np_lerp(o0[2], o1[2], a.fr_lo);
         thi = np_lerp(-o1[3], -o0[3], a.fr_hi);
       } else {
+        // yhat tails only (deterministic rows, or no trend bands requested)
         float o0[2], o1[2];
         wave_tail_select<2>(v, v, kk2, buf, o0, o1);
         if (N == 1) { o1[0] = o0[0]; o1[1] = o0[1]; }

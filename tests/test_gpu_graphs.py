@@ -71,3 +71,7 @@ def test_predict_parts_on_two_streams_equal_one_call(method):
     torch.cuda.synchronize()
     for k in one:
         assert torch.equal(one[k][:, :fg.T], two[k][:, :fg.T]), k
+    # without trend bands K5 selects only the yhat tails: same intervals
+    nc = eng.predict(fit, fg, seed=5, interval_method=method, components=False)
+    for k in ("yhat", "yhat_lower", "yhat_upper"):
+        assert torch.equal(one[k][:, :fg.T], nc[k][:, :fg.T]), k
