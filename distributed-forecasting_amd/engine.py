@@ -474,9 +474,13 @@ class FitResult:
 class Engine:
     """Batched Prophet engine bound to one GPU."""
 
-    def __init__(self, device: int = 0, config: ProphetConfig | None = None):
+    def __init__(self, device: int = 0, config: ProphetConfig | None = None,
+                 own_context: bool = False):
+        """``own_context``: a private C-ABI context (its own fit workspace), so
+        fits of this engine may run concurrently with another engine's on
+        other streams (e.g. two ForecastSteps replayed in a pipeline)."""
         self.device = device
-        self.ctx = Context.get(device)
+        self.ctx = Context(device) if own_context else Context.get(device)
         self.config = config or ProphetConfig.reference()
         self._vec_cache = {}
 
