@@ -115,23 +115,39 @@ def bucket_groups(ds_list, y_list) -> list:
     non-NaN rows is Prophet's ValueError."""
     sig_to_bucket = {}
     parts = []
+    last = None                 # (ds array, bucket) of the previous group: the common case
     for g, (ds, y) in enumerate(zip(ds_list, y_list)):
         ds = np.asarray(ds, dtype=np.int64)
         y = np.asarray(y, dtype=np.float64)
         ok = ~np.isnan(y)
-        if int(ok.sum()) < 2:
+        n_ok = int(ok.sum())
+        if n_ok < 2:
             raise ValueError("Dataframe has less than 2 non-NaN rows.")
-        order = np.argsort(ds[ok], kind="stable")
-        fds = ds[ok][order]
-        hd = np.unique(ds)
+        strictly = ds.shape[0] < 2 or bool(np.all(ds[1:] > ds[:-1]))
+        if strictly and n_ok == ds.shape[0]:
+            # sorted, unique, no NaN: fit dates = history dates = ds
+            if last is not None and last[0].shape == ds.shape and np.array_equal(last[0], ds):
+                b = last[1]
+                parts[b][2].append(y)
+                parts[b][3].append(g)
+                continue
+            fds = hd = ds
+            yv = y
+        else:
+            order = np.argsort(ds[ok], kind="stable")
+            fds = ds[ok][order]
+            hd = np.unique(ds)
+            yv = y[ok][order]
         key = (fds.tobytes(), hd.tobytes())
         b = sig_to_bucket.get(key)
         if b is None:
             b = len(parts)
             sig_to_bucket[key] = b
             parts.append((fds, hd, [], []))
-        parts[b][2].append(y[ok][order])
+        parts[b][2].append(yv)
         parts[b][3].append(g)
+        if fds is ds and hd is ds:
+            last = (ds, b)
     return [Bucket(fds, hd, np.stack(ys), np.asarray(mem, dtype=np.int64))
             for fds, hd, ys, mem in parts]
 

@@ -30,6 +30,7 @@ import uuid
 
 import numpy as np
 import pandas as pd
+import torch
 
 from . import batch as B
 from . import engine as E
@@ -153,19 +154,33 @@ class ForecastStoreItemModel:
         if logistic and "cap" not in model_input:
             raise ValueError('Capacities must be supplied for logistic growth in column "cap"')
         idx = store.index()
-        kv = np.stack([model_input["store"].to_numpy(np.int64),
-                       model_input["item"].to_numpy(np.int64)], axis=1)
+        st_col = model_input["store"].to_numpy(np.int64)
+        it_col = model_input["item"].to_numpy(np.int64)
         ds_all = B.to_ns(model_input["ds"])
         cap_all = model_input["cap"].to_numpy(np.float64) if logistic else None
-        order = np.lexsort((ds_all, kv[:, 1], kv[:, 0]))
-        sk = kv[order]
-        brk = np.flatnonzero(np.any(sk[1:] != sk[:-1], axis=1)) + 1
+        n_in = st_col.shape[0]
+        if n_in == 0:
+            return pd.DataFrame({c: pd.Series(dtype=("datetime64[ns]" if c == "ds" else np.int32
+                                                     if c in ("store", "item") else np.float32))
+                                 for c in ["ds", "store", "item", "yhat", "yhat_upper", "yhat_lower"]})
+        # rows ordered by (store, item, ds); an input already in that order
+        # (the usual layout) is not sorted again
+        code = (st_col - int(st_col.min())) * (int(it_col.max()) - int(it_col.min()) + 1) + \
+            (it_col - int(it_col.min()))
+        same = code[1:] == code[:-1]
+        if bool(np.all(code[1:] >= code[:-1])) and bool(np.all(~same | (ds_all[1:] >= ds_all[:-1]))):
+            order = np.arange(n_in)
+            sc = code
+        else:
+            order = np.lexsort((ds_all, code))
+            sc = code[order]
+        brk = np.flatnonzero(sc[1:] != sc[:-1]) + 1
         starts = np.concatenate(([0], brk))
         ends = np.concatenate((brk, [len(order)]))
         # group the groups: same record + same (sorted) dates -> one launch
         jobs = {}
         for s, e in zip(starts, ends):
-            key = tuple(sk[s].tolist())
+            key = (int(st_col[order[s]]), int(it_col[order[s]]))
             if key not in idx:
                 raise KeyError(f"no fitted model for store={key[0]} item={key[1]} "
                                f"(run_item_{key[1]}_store_{key[0]})")
@@ -177,6 +192,7 @@ class ForecastStoreItemModel:
             jobs[jk][2].append(key)
             if logistic:
                 jobs[jk][3].append(cap_all[order[s:e]])
+        cols = ["ds", "store", "item", "yhat", "yhat_upper", "yhat_lower"]
         frames = []
         for (name, _), (ds, rows, keys, caps) in jobs.items():
             fb = B.FittedBatch.from_record(eng, store.record(name), rows)
@@ -185,13 +201,14 @@ class ForecastStoreItemModel:
             n = len(rows)
             keys = np.asarray(keys, dtype=np.int64)
             fr = {"ds": np.tile(ds.astype("datetime64[ns]"), n),
-                  "store": np.repeat(keys[:, 0], Tf).astype(np.int32),
-                  "item": np.repeat(keys[:, 1], Tf).astype(np.int32)}
-            for k in ("yhat", "yhat_upper", "yhat_lower"):
-                fr[k] = out[k][:, :Tf].cpu().numpy().reshape(-1).astype(np.float32)
-            frames.append(pd.DataFrame(fr))
-        return pd.concat(frames, ignore_index=True)[
-            ["ds", "store", "item", "yhat", "yhat_upper", "yhat_lower"]]
+                  "store": np.repeat(keys[:, 0].astype(np.int32), Tf),
+                  "item": np.repeat(keys[:, 1].astype(np.int32), Tf)}
+            blk = torch.stack([out[k][:, :Tf] for k in ("yhat", "yhat_upper", "yhat_lower")]).cpu().numpy()
+            for j, k in enumerate(("yhat", "yhat_upper", "yhat_lower")):
+                fr[k] = blk[j].reshape(-1)
+            frames.append(fr)
+        return pd.DataFrame({c: (frames[0][c] if len(frames) == 1 else
+                                 np.concatenate([f[c] for f in frames])) for c in cols}, copy=False)
 
 
 _REGISTERED = {}

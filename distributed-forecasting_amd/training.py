@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import numpy as np
 import pandas as pd
+import torch
 
 from . import batch as B
 from . import engine as E
@@ -116,13 +117,34 @@ def group_frame(df: pd.DataFrame, keys):
     """Split a long frame into groups (original row order kept inside each
     group, like the frames applyInPandas hands to the UDF).
     Returns (group keys [G, k] int64, list of row-position arrays)."""
-    kv = np.stack([df[k].to_numpy(np.int64) for k in keys], axis=1)
-    order = np.lexsort(kv.T[::-1])                  # stable: keeps row order in a group
-    sk = kv[order]
-    brk = np.flatnonzero(np.any(sk[1:] != sk[:-1], axis=1)) + 1
+    cols = [df[k].to_numpy(np.int64) for k in keys]
+    n = cols[0].shape[0] if cols else 0
+    if n == 0:
+        return np.zeros((0, len(keys)), np.int64), []
+    # one sortable code per row when the keys fit (store / item ids): a
+    # frame already grouped (the usual layout of the sales table) needs no
+    # sort at all; otherwise one stable argsort of the codes
+    lo = [int(c.min()) for c in cols]
+    span = [int(c.max()) - l + 1 for c, l in zip(cols, lo)]
+    if float(np.prod(np.asarray(span, np.float64))) < 2.0 ** 62:
+        code = cols[0] - lo[0]
+        for c, l, sp in zip(cols[1:], lo[1:], span[1:]):
+            code = code * sp + (c - l)
+        if bool(np.all(code[1:] >= code[:-1])):
+            order, sc = np.arange(n), code
+        else:
+            order = np.argsort(code, kind="stable")
+            sc = code[order]
+        brk = np.flatnonzero(sc[1:] != sc[:-1]) + 1
+    else:
+        kv = np.stack(cols, axis=1)
+        order = np.lexsort(kv.T[::-1])              # stable: keeps row order in a group
+        sk = kv[order]
+        brk = np.flatnonzero(np.any(sk[1:] != sk[:-1], axis=1)) + 1
     starts = np.concatenate(([0], brk))
-    ends = np.concatenate((brk, [len(order)]))
-    return sk[starts], [order[s:e] for s, e in zip(starts, ends)]
+    ends = np.concatenate((brk, [n]))
+    first = order[starts]
+    return np.stack([c[first] for c in cols], axis=1), [order[s:e] for s, e in zip(starts, ends)]
 
 
 def forecast_store_items(df: pd.DataFrame, keys=("store", "item"), *, periods: int = HORIZON_DAYS,
@@ -151,22 +173,23 @@ def forecast_store_items(df: pd.DataFrame, keys=("store", "item"), *, periods: i
     frames, fits = [], []
 
     def emit(bk, fut, host):
-        # one bucket's rows of the output frame (schema of 02_training.py:307)
+        # one bucket's rows of the output frame (schema of 02_training.py:307),
+        # as column arrays; the frame is built once at the end
         bkeys = gkeys[bk.members]
         Tf = len(fut)
         n = len(bk.members)
-        yin = np.full((n, Tf), np.nan)
+        yin = np.full((n, Tf), np.nan, np.float32)
         for i, g in enumerate(bk.members):
             v = y_list[g]
             m = min(Tf, len(v))
             yin[i, :m] = v[:m]
         fr = {"ds": np.tile(fut.astype("datetime64[ns]"), n)}
         for j, k in enumerate(keys):
-            fr[k] = np.repeat(bkeys[:, j], Tf).astype(np.int32)
-        fr["y"] = yin.reshape(-1).astype(np.float32)
+            fr[k] = np.repeat(bkeys[:, j].astype(np.int32), Tf)
+        fr["y"] = yin.reshape(-1)
         for k in ("yhat", "yhat_upper", "yhat_lower"):
-            fr[k] = host[k][:, :Tf].reshape(-1).astype(np.float32)
-        frames.append(pd.DataFrame(fr))
+            fr[k] = np.ascontiguousarray(host[k][:, :Tf], dtype=np.float32).reshape(-1)
+        frames.append(fr)
 
     # buckets with compatible layouts (seasonalities, changepoint count) but
     # different date grids share one ragged launch
@@ -178,7 +201,8 @@ def forecast_store_items(df: pd.DataFrame, keys=("store", "item"), *, periods: i
                                          series_ids=B.series_id(bkeys))
             fut = B.future_dates(bk.history_dates, periods, freq, include_history=True)
             Tf, out = fb.predict(fut, seed=seed, components=False)
-            emit(bk, fut, {k: out[k][:, :Tf].cpu().numpy() for k in ("yhat", "yhat_upper", "yhat_lower")})
+            blk = torch.stack([out[k][:, :Tf] for k in ("yhat", "yhat_upper", "yhat_lower")]).cpu().numpy()
+            emit(bk, fut, {k: blk[j] for j, k in enumerate(("yhat", "yhat_upper", "yhat_lower"))})
             subs = [(bkeys, fb)]
         else:
             bks = [buckets[b] for b in pack]
@@ -186,7 +210,8 @@ def forecast_store_items(df: pd.DataFrame, keys=("store", "item"), *, periods: i
             rb = B.RaggedFittedBatch.fit_buckets(eng, bks, series_ids=B.series_id(pkeys))
             futs = rb.future(periods, freq)
             _, out = rb.predict(futs, seed=seed, components=False)
-            host = {k: out[k].cpu().numpy() for k in ("yhat", "yhat_upper", "yhat_lower")}
+            blk = torch.stack([out[k] for k in ("yhat", "yhat_upper", "yhat_lower")]).cpu().numpy()
+            host = {k: blk[j] for j, k in enumerate(("yhat", "yhat_upper", "yhat_lower"))}
             subs = []
             for j, bk in enumerate(bks):
                 r0, r1 = int(rb.row0[j]), int(rb.row0[j + 1])
@@ -198,10 +223,13 @@ def forecast_store_items(df: pd.DataFrame, keys=("store", "item"), *, periods: i
             if return_fits:
                 fits.append((bkeys, fb))
     cols = ["ds"] + keys + ["y", "yhat", "yhat_upper", "yhat_lower"]
-    res = (pd.concat(frames, ignore_index=True) if frames else
-           pd.DataFrame({c: pd.Series(dtype=("datetime64[ns]" if c == "ds" else
-                                              np.int32 if c in keys else np.float32))
-                         for c in cols}))[cols]
+    if frames:
+        res = pd.DataFrame({c: (frames[0][c] if len(frames) == 1 else
+                                np.concatenate([f[c] for f in frames])) for c in cols}, copy=False)
+    else:
+        res = pd.DataFrame({c: pd.Series(dtype=("datetime64[ns]" if c == "ds" else
+                                                 np.int32 if c in keys else np.float32))
+                            for c in cols})
     return (res, fits) if return_fits else res
 
 
