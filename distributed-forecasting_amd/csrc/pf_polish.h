@@ -502,11 +502,19 @@ __device__ __forceinline__ void sweep_in_free(const FitKArgs &a, FitSmem<NW, KMA
       for (int h = 0; h < PW; ++h) {
         const int j = lane + 64 * h;
         if (j < P) {
-          double *Ar = A + r0 * LDl + j;
+          // this wave's rows: every load issued before the first store (one
+          // LDS latency per pivot instead of one per row); rows past P read
+          // row P - 1 and are not stored; row k is left for wave 0 below
+          double av[RW];
+#pragma unroll
+          for (int q = 0; q < RW; ++q) {
+            const int i = min(r0 + q, P - 1);
+            av[q] = A[i * LDl + j];
+          }
 #pragma unroll
           for (int q = 0; q < RW; ++q) {
             const int i = r0 + q;
-            if (i < P && i != k) Ar[q * LDl] = fma(-pv_read<PW>(akj, i), sj[h], Ar[q * LDl]);
+            if (i < P && i != k) A[i * LDl + j] = fma(-pv_read<PW>(akj, i), sj[h], av[q]);
           }
         }
       }
