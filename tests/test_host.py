@@ -340,3 +340,38 @@ def test_ragged_packs_group_by_layout():
     # count splits
     packs = B.ragged_packs(bks, ProphetConfig.reference())
     assert sorted(len(p) for p in packs) == [1, 5], packs
+
+
+def test_group_frame_and_buckets_fast_paths():
+    """group_frame's integer-code path (sorted input: no sort; shuffled input:
+    one stable argsort) and bucket_groups' sorted fast path give the same
+    groups, row order and buckets as the general path."""
+    import numpy as np
+    import pandas as pd
+    from distributed_forecasting_amd import batch as B, synthetic, training
+    df = synthetic.store_item_frame(3, 4, start="2016-01-01", end="2016-03-31")
+    g0, r0 = training.group_frame(df, ["store", "item"])
+    sh = df.sample(frac=1.0, random_state=1)
+    g1, r1 = training.group_frame(sh, ["store", "item"])
+    assert np.array_equal(g0, g1) and len(r0) == len(r1) == 12
+    idx = sh.index.to_numpy()
+    for a, b in zip(r1, r0):
+        assert np.all(np.diff(a) > 0)                       # stable: input order kept
+        assert np.array_equal(np.sort(idx[a]), b)
+    # keys beyond the integer-code range take the lexsort path
+    big = df.assign(store=df["store"].astype(np.int64) * (1 << 40))
+    g2, r2 = training.group_frame(big, ["store", "item"])
+    assert np.array_equal(g2[:, 1], g0[:, 1]) and all(np.array_equal(a, b) for a, b in zip(r2, r0))
+    # buckets: sorted NaN-free groups (fast path) vs the same groups reversed
+    ds = B.to_ns(df["ds"])
+    y = df["y"].to_numpy(np.float64)
+    fwd = B.bucket_groups([ds[r] for r in r0], [y[r] for r in r0])
+    rev = B.bucket_groups([ds[r][::-1] for r in r0], [y[r][::-1] for r in r0])
+    assert len(fwd) == len(rev) == 1
+    assert np.array_equal(fwd[0].fit_ds, rev[0].fit_ds) and np.array_equal(fwd[0].Y, rev[0].Y)
+    assert np.array_equal(fwd[0].members, rev[0].members)
+    yn = [y[r].copy() for r in r0]
+    yn[2][5] = np.nan
+    mixed = B.bucket_groups([ds[r] for r in r0], yn)
+    assert len(mixed) == 2 and sorted(len(b.members) for b in mixed) == [1, 11]
+    assert pd.Series([b.fit_ds.shape[0] for b in mixed]).isin([90, 91]).all()
