@@ -408,6 +408,11 @@ __device__ __forceinline__ PV<PW> pv_zero() {
   return r;
 }
 
+// a warm-up pass (pf_fit_opts.lbfgs_warmup_evals > 0) ends at its next accepted
+// iterate once it has used that many evaluations, or inside a line search at
+// the last accepted iterate once it has used PF_WARM_LS_SLACK more
+#define PF_WARM_LS_SLACK 10
+
 struct FitKArgs {
   int T, Tp, K, S, growth, P, NB;
   const double *t, *XT, *t_change;
@@ -1257,6 +1262,11 @@ __device__ __forceinline__ bool lbfgs_step(const pf_fit_opts &o, LbLds<PW> &L, i
         state = LB_TRY;
         break;
       case LB_TRY:
+        if (o.lbfgs_warmup_evals > 0 && z.n_eval >= o.lbfgs_warmup_evals + PF_WARM_LS_SLACK) {
+          // warm-up pass out of evaluations inside a line search: end it at
+          // the last accepted iterate (the polish takes it from there)
+          z.ret = PF_ST_MAXIT; state = LB_DONE; return false;
+        }
         if (z.nits >= 20) { state = LB_LS_FAIL; break; }
 #pragma unroll
         for (int h = 0; h < PW; ++h) xq[h] = xk[h] + z.alpha1 * pk[h];
@@ -1298,6 +1308,9 @@ __device__ __forceinline__ bool lbfgs_step(const pf_fit_opts &o, LbLds<PW> &L, i
         break;
       }
       case LB_ZOOM_ITER: {
+        if (o.lbfgs_warmup_evals > 0 && z.n_eval >= o.lbfgs_warmup_evals + PF_WARM_LS_SLACK) {
+          z.ret = PF_ST_MAXIT; state = LB_DONE; return false;
+        }
         z.zit++;
         if (fabs(z.alo - z.ahi) < 1e-16) { state = LB_LS_FAIL; break; }
         if (z.zit % 5 == 0) {

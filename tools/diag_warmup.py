@@ -44,7 +44,7 @@ def run(**opt):
     return worse, np.mean(ms), np.mean(nem), np.max(nex)
 
 
-for W, WE in ((60, 0), (50, 0), (40, 0), (60, 90), (60, 100), (60, 110), (50, 80), (45, 70)):
+for W, WE in ((60, 90), (60, 80), (50, 80), (60, 0)):
     w, ms, nem, nex = run(lbfgs_warmup=W, lbfgs_warmup_evals=WE)
     print(f"warmup {W:3d} iters, {WE:3d} evals: worse basin than stan_map {w:2d} / 2000; "
           f"fit {ms:.3f} ms per 500; n_eval mean {nem:.1f} max {nex}", flush=True)
