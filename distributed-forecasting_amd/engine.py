@@ -285,6 +285,7 @@ class RaggedGrid:
         self.Ts = np.asarray([g.T for g in grids], np.int64)
         self.T = int(self.Ts.max())
         self.packed = None
+        self.device = device
         self._set_grid_of(grid_of, device)
         arr = (L.PfGrid * self.G)(*[g.as_pf() for g in grids])
         self.table = _to_device_async(np.frombuffer(bytes(arr), np.uint8).copy(),
@@ -816,8 +817,12 @@ class Engine:
         rc = self.ctx.lib.pf_predict(self.ctx.h, ctypes.byref(a), ctypes.c_void_p(mc_stream.cuda_stream))
         self.ctx.check(rc, "pf_predict (mc part)")
         if not torch.cuda.is_current_stream_capturing():
-            # (a captured graph's pool keeps its blocks for the graph's life)
-            for v in list(out.values()) + [fit.theta, fit.y_scale]:
+            # everything K5 reads or writes stays allocated until it ran on the
+            # side stream (a captured graph's pool keeps its blocks anyway)
+            fgt = fgrid.tensors() if isinstance(fgrid, RaggedGrid) else \
+                [fgrid.t, fgrid.XT, fgrid.t_change, fgrid.seg]
+            extra = [t for t in (series_id, cap_s) if t is not None]
+            for v in list(out.values()) + [fit.theta, fit.y_scale] + fgt + extra:
                 v.record_stream(mc_stream)
         a.parts = L.PF_PREDICT_DET
         rc = self.ctx.lib.pf_predict(self.ctx.h, ctypes.byref(a), _stream(self.device))
