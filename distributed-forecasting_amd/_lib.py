@@ -18,7 +18,7 @@ STATUS_NAMES = {0: "SUCCESS", 10: "ABSX", 20: "ABSF", 21: "RELF", 30: "ABSGRAD",
                 60: "WARMUP", 70: "MAP"}
 PF_ST_CONSTANT = 50
 
-# Every symbol include/prophet_hip.h declares (checked by tests/test_abi.py).
+# Every symbol include/prophet_hip.h declares (checked by tests/test_host.py).
 EXPORTED = ["pf_ctx_create", "pf_ctx_destroy", "pf_last_error", "pf_default_fit_opts",
             "pf_num_changepoints", "pf_build_grid", "pf_prepare", "pf_objective_grad",
             "pf_fit", "pf_predict", "pf_set_timing", "pf_read_timings", "pf_cv_metrics",
