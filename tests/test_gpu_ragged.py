@@ -177,3 +177,17 @@ def test_ragged_irregular_grids_and_layout_split():
         assert np.array_equal(a[c].to_numpy(), b[c].to_numpy()), c
     ya, yb = a["yhat"].to_numpy(np.float64), b["yhat"].to_numpy(np.float64)
     assert np.max(np.abs(ya - yb) / np.maximum(1.0, np.abs(yb))) <= 1e-5
+
+
+def test_ragged_never_takes_the_tile_path():
+    """K3T needs one grid per tile: a ragged batch with tile_min_series=1 runs
+    the per-series kernels and gives the same fits as the default."""
+    e = dfa.Engine(0, ProphetConfig.reference())
+    _, _, bks = _buckets(1, 20, n_starts=3, n_ends=1)
+    rb = B.RaggedFittedBatch.fit_buckets(e, bks)
+    rg = rb.fit.grid
+    Yd = torch.zeros((rb.n, rg.T_pad), dtype=torch.float64, device="cuda")
+    for j, bk in enumerate(bks):
+        Yd[int(rb.row0[j]):int(rb.row0[j + 1]), :bk.fit_ds.shape[0]] = torch.from_numpy(bk.Y).cuda()
+    f1 = e.fit(rg, Yd, tile_min_series=1)
+    assert torch.equal(f1.theta, rb.fit.theta) and torch.equal(f1.status, rb.fit.status)
