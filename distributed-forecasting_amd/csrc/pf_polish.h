@@ -90,6 +90,16 @@ __device__ __forceinline__ void hessian_collective(const FitKArgs &a, FitSmem<NW
   double *Mt = sm.pmt;    // [32][32] d m_s / d theta_c (logistic)
   double *rho = sm.prho;  // [32]     sum_{i in s} r u cap s'
   publish_theta<NW, KMAX, MODE>(a, sm, x);
+  // logistic: per row-group partial segment sums rho in U ([16][32]; U is
+  // free while the Hessian is rebuilt: the previous swept matrix is dead).
+  // Each row group (wave, rq) visits every segment in one run and writes its
+  // sum once; the totals are added in a fixed order below (bitwise
+  // reproducible, no atomics)
+  double *rslot = sm.U;
+  if constexpr (logistic) {
+    static_assert(NW <= 4, "rho slots: 4 row groups per wave, 16 slots");
+    for (int e = threadIdx.x; e < 16 * 32; e += NW * 64) rslot[e] = 0.0;
+  }
   if constexpr (logistic) {
     if (wave == 0) {
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -209,7 +219,7 @@ __device__ __forceinline__ void hessian_collective(const FitKArgs &a, FitSmem<NW
       // rho_s: one lane per row, flushed to LDS when the (monotone) segment changes
       if (c16 == 0 && valid) {
         if (sg != cur_seg) {
-          if (rho_acc != 0.0) atomicAdd(&rho[cur_seg], rho_acc);
+          rslot[(wave * 4 + rq) * 32 + cur_seg] = rho_acc;
           rho_acc = 0.0;
           cur_seg = sg;
         }
@@ -231,7 +241,15 @@ __device__ __forceinline__ void hessian_collective(const FitKArgs &a, FitSmem<NW
     mfma_tiles<0, NB, NT, NBB>(acc, lt, rt, gt, V, W);
   }
   if constexpr (logistic) {
-    if (c16 == 0 && rho_acc != 0.0) atomicAdd(&rho[cur_seg], rho_acc);
+    if (c16 == 0) rslot[(wave * 4 + rq) * 32 + cur_seg] = rho_acc;
+    __syncthreads();
+    if (threadIdx.x < 32) {
+      double tot = 0.0;
+#pragma unroll
+      for (int g2 = 0; g2 < 16; ++g2) tot += rslot[g2 * 32 + threadIdx.x];
+      rho[threadIdx.x] = tot;
+    }
+    __syncthreads();  // U becomes the tile-reduction buffer below
   }
   // ---- chained reduction of the tiles over waves through one LDS buffer
   Q = wave_sum(Q);

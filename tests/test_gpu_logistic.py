@@ -166,3 +166,27 @@ def test_prophet_class_logistic():
     assert np.max(np.abs(fc["yhat"].to_numpy() - pt["yhat"])) <= 1e-5 * ysc
     assert np.all(fc["trend"].to_numpy() <= fut["cap"].to_numpy() * (1 + 1e-6))
     assert "cap_scaled" in m.history
+
+
+def test_logistic_fit_is_bitwise_reproducible():
+    """The logistic polish Hessian's segment sums are added in a fixed order
+    (no atomics): two fits of the same batch give identical theta."""
+    import torch
+    import distributed_forecasting_amd as dfa
+    from distributed_forecasting_amd import synthetic
+    from distributed_forecasting_amd.engine import ProphetConfig
+    cfg = ProphetConfig.reference()
+    cfg.growth = "logistic"
+    ds = synthetic.daily_dates("2015-01-01", "2017-12-31")
+    Y, cap = synthetic.saturating_matrix(24, ds)
+    e = dfa.Engine(0, cfg)
+    seasons = cfg.seasons(int(ds[0]), int(ds[-1]), int(ds[1] - ds[0]))
+    g = dfa.build_grid(ds, seasons, start_ns=int(ds[0]), t_scale_ns=int(ds[-1] - ds[0]))
+    Yd = torch.zeros((24, g.T_pad), dtype=torch.float64, device="cuda")
+    Yd[:, :g.T] = torch.from_numpy(Y).cuda()
+    cd = torch.zeros_like(Yd)
+    cd[:, :g.T] = torch.from_numpy(cap).cuda()
+    f1 = e.fit(g, Yd, cap=cd)
+    f2 = e.fit(g, Yd, cap=cd)
+    assert torch.equal(f1.theta, f2.theta) and torch.equal(f1.f, f2.f)
+    assert bool((f1.status == 70).all())
