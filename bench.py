@@ -242,22 +242,23 @@ def main():
             k[1] += 1
         return {k: v[0] / v[1] for k, v in kern.items()}
 
-    def timed(fn, steps, warm=1):
+    def timed(fn, steps, warm=1, ctx=None):
         """Same bracketing as the headline: warm-up, barrier + sync, `steps`
-        calls, barrier + sync, max over ranks; kernel averages from the
-        engine's HIP events."""
+        calls, barrier + sync, max over ranks; kernel averages from the HIP
+        events of the engine context the launches go through."""
+        ctx = ctx or eng.ctx
         for _ in range(warm):
             fn()
         bracket()
-        eng.ctx.set_timing(True)
+        ctx.set_timing(True)
         t0_ = time.perf_counter()
         r = None
         for _ in range(steps):
             r = fn()
         bracket()
         el = time.perf_counter() - t0_
-        ka = averages(eng.ctx.read_timings())
-        eng.ctx.set_timing(False)
+        ka = averages(ctx.read_timings())
+        ctx.set_timing(False)
         return max_over_ranks(el), ka, r
 
     # ---------------------------------------------------------- headline
@@ -279,11 +280,12 @@ def main():
                                     counts=counts)
         return r
 
-    el_eager, kern_avg, _ = timed(lambda: gather(fstep.run()), args.steps, args.warmup)
+    sctx = fstep.engine.ctx                 # the step's private context (graphs.py)
+    el_eager, kern_avg, _ = timed(lambda: gather(fstep.run()), args.steps, args.warmup, sctx)
     launch = "hipGraph replay"
     try:
         fstep.capture()
-        elapsed, _, r = timed(lambda: gather(fstep.replay()), args.steps, args.warmup)
+        elapsed, _, r = timed(lambda: gather(fstep.replay()), args.steps, args.warmup, sctx)
     except Exception as e:                  # capture unsupported: report the eager step
         launch = f"eager (graph capture failed: {type(e).__name__}: {e})"
         elapsed, r = el_eager, fstep.run()
@@ -450,19 +452,41 @@ def dropin(args, eng, keys, ds, Y, Yd, rank, world, bracket, max_over_ranks, sum
     tot = sum_over_ranks(n)
     out = {}
 
-    def fsi():
-        fr = dfa.forecast_store_items(df, device=int(device.index))
+    def fsi(cv=False):
+        # df holds this rank's shard already
+        r = dfa.forecast_store_items(df, device=int(device.index), cv_metrics=cv,
+                                     return_metrics=cv)
+        fr, met = r if cv else (r, None)
         if world > 1:
             fr = parallel.gather_frames(fr, device=device)
-        return fr
-    el, ka, fr = timed(fsi, steps)
+            if cv:
+                import torch
+                mt = torch.from_numpy(met[list(dfa.CV_METRICS)].to_numpy()).to(device)
+                kt = torch.from_numpy(met[["store", "item"]].to_numpy(np.int64)).to(device)
+                g = parallel.gather_results(kt, None, mt)
+                met = g["metrics"]
+        return fr, met
+    el, ka, (fr, _) = timed(fsi, steps)
     out["forecast_store_items"] = {
         "value": tot * steps / el, "unit": "series/s", "ms_per_call": el / steps * 1e3,
         "rows_out": int(len(fr)),
         "note": "groupBy('store','item').applyInPandas(forecast_store_item) equivalent "
                 "(02_training.py:305-307): long pandas frame in (913k rows at 500 series), "
                 "[ds, store, item, y, yhat, yhat_upper, yhat_lower] frame out (float32, int32 "
-                "keys); grouping, grid bucketing, H2D/D2H and frame assembly included"}
+                "keys); grouping, grid bucketing, H2D/D2H and frame assembly included; N>1: "
+                "this rank's hash shard + tensor all-gather of the frames"}
+    el, ka, (fr, met) = timed(lambda: fsi(True), steps)
+    out["forecast_store_items_cv"] = {
+        "value": tot * steps / el, "unit": "series/s", "ms_per_call": el / steps * 1e3,
+        "kernels_ms": ka,
+        "cv_metric_means": {k: float(np.nanmean(np.asarray(met[k] if hasattr(met, "columns") else
+                                                           met[:, i].cpu().numpy())))
+                            for i, k in enumerate(dfa.CV_METRICS[:4])},
+        "note": "forecast_store_items(cv_metrics=True): the reference's train_model always runs "
+                "cross_validation(horizon 90d, period 360d, initial 730d) + performance_metrics "
+                "(02_training.py:178-188) — 3 fold refits + fold forecasts + K6 per bucket on "
+                "the GPU, per-series mse/rmse/mae/mape returned (N>1: RCCL all-gather of the CV "
+                "metrics with the keys)"}
     with tempfile.TemporaryDirectory() as tmp:
         store = dfa.ParamsStore(os.path.join(tmp, "params"), writer=f"r{rank}")
         dfa.forecast_store_items(df, params_store=store, device=int(device.index))
@@ -485,7 +509,14 @@ def dropin(args, eng, keys, ds, Y, Yd, rank, world, bracket, max_over_ranks, sum
                               device=int(device.index))
         fit = eng.fit(grid, Yd)
         fg = eng.predict_grid(fit, dfa.future_dates(ds, HORIZON))
-        return met, eng.predict(fit, fg, seed=0, components=False)
+        o = eng.predict(fit, fg, seed=0, components=False)
+        if world > 1:
+            # the exchange north_star names: keys, forecasts and the CV metrics
+            blk = torch.stack([o["yhat"], o["yhat_lower"], o["yhat_upper"]], 1)
+            parallel.gather_results(kd_local, blk, met[:, :4].contiguous(), fit.status)
+        return met, o
+    import torch
+    kd_local = torch.from_numpy(keys.astype(np.int64)).to(device)
     el, ka, _ = timed(cv_on, steps)
     out["cv_on"] = {
         "value": tot * steps / el, "unit": "series/s", "ms_per_step": el / steps * 1e3,
@@ -493,7 +524,8 @@ def dropin(args, eng, keys, ds, Y, Yd, rank, world, bracket, max_over_ranks, sum
         "note": "train_model with its cross_validation(horizon='90 days', period='360 days', "
                 "initial='730 days') + performance_metrics (02_training.py:178-188): 3 fold refits "
                 "(1016/1376/1736 rows) + fold forecasts + K6, then the full fit + 90-day forecast "
-                "with intervals; the headline value is the CV-off figure"}
+                "with intervals; N>1: RCCL all-gather of keys, forecasts and the CV metrics; the "
+                "headline value is the CV-off figure"}
     return out
 
 

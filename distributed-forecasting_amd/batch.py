@@ -286,7 +286,8 @@ class FittedBatch:
         if isinstance(Y, torch.Tensor):
             Yd[:, :T] = Y[:, :T].to(dev, torch.float64)
         else:
-            Yd[:, :T] = torch.from_numpy(np.ascontiguousarray(Y, dtype=np.float64)).to(dev)
+            # pinned staging: the H2D runs asynchronously (no pageable stall)
+            Yd[:, :T] = E._to_device_async(np.asarray(Y, dtype=np.float64), dev)
         capd = None
         if cfg.growth == "logistic":
             if cap is None:

@@ -423,9 +423,10 @@ struct FitKArgs {
   int R, TQ;                 // rows per thread, TQ = NL*R
   const double *tP, *XTP;    // [TQ], [K][TQ]
   const int32_t *sgP;        // [TQ] seg | (#changepoints first active at this row) << 16
-  // row-major copy of the features for the tiled kernel K3T: [Tp][32],
-  // features >= K zero (NULL unless the tiled path may run)
+  // row-major copy of the features for the tiled kernel K3T: [Tp][XR_width]
+  // (32 or 48), features >= K zero (NULL unless the tiled path may run)
   const double *XR;
+  int XR_width;
   const double *sigmas, *s_a, *s_m;
   double tau;
   // hyperparameter batching: per-series prior scales (NULL: the shared
@@ -2300,12 +2301,13 @@ __global__ __launch_bounds__(256) void k_permute_grid_ragged(const pf_grid *__re
   for (int f = 0; f < K; ++f) XTP[(size_t)f * TQ + q] = v ? XT[(size_t)f * Tp + i] : 0.0;
 }
 
-// Row-major feature copy for K3T: XR[r][f] = X[r][f] (f < K), 0 for K <= f < 32.
+// Row-major feature copy for K3T: XR[r][f] = X[r][f] (f < K), 0 for K <= f < W
+// (W = 32 or 48, the tile's padded feature count).
 __global__ __launch_bounds__(256) void k_grid_rowmajor(const double *__restrict__ XT, int Tp, int K,
-                                                       double *__restrict__ XR) {
+                                                       int W, double *__restrict__ XR) {
   const size_t q = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (q >= (size_t)Tp * 32) return;
-  const int r = (int)(q >> 5), f = (int)(q & 31);
+  if (q >= (size_t)Tp * W) return;
+  const int r = (int)(q / W), f = (int)(q - (size_t)r * W);
   XR[q] = f < K ? XT[(size_t)f * Tp + r] : 0.0;
 }
 
@@ -2395,16 +2397,17 @@ int launch_fitlike(pf_ctx *ctx, int what, const FitKArgs &a, int n, hipStream_t 
       caps[0] = a.o.max_iter; warm[0] = 0;
     }
     // tiled first pass (K3T, 16 series per workgroup, MFMA row pass) for
-    // large batches of the layouts it covers; the per-series kernels finish
-    constexpr bool TILE_OK = (MODE & (PF_MODE_LOGI | PF_MODE_WIDE)) == 0 && KMAX <= 32;
+    // large batches of the layouts it covers (K <= 48, P <= 72, S + 1 <= 32,
+    // shared prior scales, one grid); the per-series kernels finish
+    constexpr int TKP = KMAX <= 32 ? 32 : 48;
+    constexpr bool TILE_OK = KMAX <= 48;
     bool tile = false;
     size_t smem_t = 0;
     if constexpr (TILE_OK) {
-      smem_t = TileSmem<MODE>::bytes();
-      tile = a.o.tile_min_series >= 0 && n >= a.o.tile_min_series && a.P <= PF_TV && a.K <= 32 &&
-             a.S + 1 <= 32 && a.growth != PF_GROWTH_LOGISTIC && !a.tau_series && !a.sigmas_series && a.XR &&
-             !a.grid_of &&
-             smem_t <= 160 * 1024;
+      smem_t = TileSmem<MODE, TKP>::bytes();
+      tile = a.o.tile_min_series >= 0 && n >= a.o.tile_min_series && a.P <= TileTr<MODE, TKP>::TV &&
+             a.K <= TKP && a.S + 1 <= 32 && !a.tau_series && !a.sigmas_series && a.XR &&
+             a.XR_width == TKP && !a.grid_of && smem_t <= 160 * 1024;
     }
     if (npass == 3 && !tile && !getenv_flag("PF_SPLIT_POLISH")) {
       if constexpr (HAS_POLISH) {
@@ -2426,7 +2429,7 @@ int launch_fitlike(pf_ctx *ctx, int what, const FitKArgs &a, int n, hipStream_t 
       const int v = ps == 0 ? 0 : 1;
       if (ps == 0 && tile) {
         if constexpr (TILE_OK) {
-          auto kt = k_fit_tile<MODE>;
+          auto kt = k_fit_tile<MODE, TKP>;
           PF_HIP(ctx, hipFuncSetAttribute((const void *)kt, hipFuncAttributeMaxDynamicSharedMemorySize,
                                           (int)smem_t));
           const int nt = (n + PF_TS - 1) / PF_TS;
@@ -2526,7 +2529,8 @@ static int prepare_fit_scratch(pf_ctx *ctx, FitKArgs &a, hipStream_t st, bool ro
     PF_HIP(ctx, hipGetLastError());
     return 0;
   }
-  const size_t rbytes = rowmajor ? (size_t)a.Tp * 32 * sizeof(double) : 0;
+  const int W = a.K <= 32 ? 32 : 48;
+  const size_t rbytes = rowmajor ? (size_t)a.Tp * W * sizeof(double) : 0;
   void *w = nullptr;
   const int rc = ctx_workspace(ctx, gbytes + rbytes, &w);
   if (rc) return rc;
@@ -2535,6 +2539,7 @@ static int prepare_fit_scratch(pf_ctx *ctx, FitKArgs &a, hipStream_t st, bool ro
   a.XTP = base + TQ;
   a.sgP = (int32_t *)(base + TQ * (1 + (size_t)a.K));
   a.XR = nullptr;
+  a.XR_width = 0;
   const int nb = (int)((TQ + 255) / 256);
   PF_TIMED_LAUNCH(ctx, "k_permute_grid", nb, st, k_permute_grid, dim3(nb), dim3(256), 0, st,
                   a.t, a.seg, a.XT, a.T, a.Tp, a.K, a.S, a.R, PF_FIT_NW * 64,
@@ -2543,11 +2548,12 @@ static int prepare_fit_scratch(pf_ctx *ctx, FitKArgs &a, hipStream_t st, bool ro
   PF_HIP(ctx, hipGetLastError());
   if (rowmajor) {
     double *xr = (double *)((char *)w + gbytes);
-    const int nr = (int)(((size_t)a.Tp * 32 + 255) / 256);
+    const int nr = (int)(((size_t)a.Tp * W + 255) / 256);
     PF_TIMED_LAUNCH(ctx, "k_grid_rowmajor", nr, st, k_grid_rowmajor, dim3(nr), dim3(256), 0, st,
-                    a.XT, a.Tp, a.K, xr);
+                    a.XT, a.Tp, a.K, W, xr);
     PF_HIP(ctx, hipGetLastError());
     a.XR = xr;
+    a.XR_width = W;
   }
   return 0;
 }
@@ -2607,7 +2613,8 @@ int pf_fit(pf_ctx *ctx, const pf_problem *pb, const pf_fit_opts *opts, double *t
   a.o = *opts;
   // the tiled first pass reads a row-major feature copy
   const bool maybe_tile = opts->tile_min_series >= 0 && pb->n_series >= opts->tile_min_series &&
-                          pb->grid.K <= 32 && pb->n_grids == 0;
+                          pb->grid.K <= 48 && pb->n_grids == 0 && !pb->tau_series &&
+                          !pb->sigmas_series;
   rc = prepare_fit_scratch(ctx, a, (hipStream_t)stream, maybe_tile, pb->n_grids);
   if (rc) return rc;
   return dispatch_fitlike(ctx, PF_LAUNCH_FIT, a, pb->n_series, pb->fourier_orders, mode_of(pb),

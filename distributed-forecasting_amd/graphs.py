@@ -11,8 +11,13 @@ every replay over whatever is in the static input buffer ``Y`` (refresh it
 with ``set_inputs``); only the host-side launch work is recorded.
 
 Capture needs the engine's context workspace to be allocated already (no
-hipMalloc while capturing): the constructor runs the step once eagerly
-first.  RCCL collectives stay outside the graph (run them after replay).
+hipMalloc while capturing): ``capture`` runs the step once eagerly first.
+The captured kernels keep pointers into that workspace (the fit's grid
+copies), so a step never shares it: when the engine given uses the
+per-device shared context, the step runs on a private engine (same config,
+its own C-ABI context) — a later, larger fit elsewhere cannot reallocate
+the buffers a graph replays on.  RCCL collectives stay outside the graph
+(run them after replay).
 """
 from __future__ import annotations
 
@@ -34,6 +39,8 @@ class ForecastStep:
                  freq_ns: int = E.NS_PER_DAY, series_id: torch.Tensor | None = None,
                  seed: int = 0, metrics: bool = True, interval_method: str | None = None,
                  components: bool = False):
+        if E.Context._by_device.get(engine.device) is engine.ctx:
+            engine = E.Engine(engine.device, engine.config, own_context=True)
         self.engine = engine
         cfg = engine.config
         self.ds = np.asarray(ds_ns, np.int64)

@@ -55,7 +55,7 @@ def gather_blocks(local: torch.Tensor, counts=None):
     return torch.cat(parts, 0), counts
 
 
-def gather_results(keys: torch.Tensor, forecast: torch.Tensor, metrics: torch.Tensor | None = None,
+def gather_results(keys: torch.Tensor, forecast: torch.Tensor | None, metrics: torch.Tensor | None = None,
                    status: torch.Tensor | None = None, counts=None) -> dict:
     """The engine's final exchange: every rank's
     [S_g, k] int64 series keys, [S_g, 3, T] fp32 forecast blocks (yhat,
@@ -66,7 +66,8 @@ def gather_results(keys: torch.Tensor, forecast: torch.Tensor, metrics: torch.Te
         counts = gather_counts(keys.shape[0], keys.device)
     out = {"counts": counts}
     out["keys"], _ = gather_blocks(keys, counts)
-    out["forecast"], _ = gather_blocks(forecast, counts)
+    if forecast is not None:
+        out["forecast"], _ = gather_blocks(forecast, counts)
     if metrics is not None:
         out["metrics"], _ = gather_blocks(metrics, counts)
     if status is not None:

@@ -19,7 +19,8 @@ written to a private temporary name and moved into place atomically), and the
 index is a scan of the directory — there is no shared mutable manifest.
 ``manifest.json`` holds only the store's model configuration, written once
 when the store is created (identical content from every creator).  Later
-records win for a key that was refitted (names sort by creation time).
+records win for a key that was refitted (names sort by generation: the
+writer's clock unless the caller passes one, see ``ParamsStore``).
 """
 from __future__ import annotations
 
@@ -38,10 +39,35 @@ from .forecaster import get_engine
 
 MANIFEST = "manifest.json"
 REC_PREFIX = "rec_"
+LEGACY_PREFIX = "bucket_"
+# ProphetConfig fields that change what a stored fit means (its parameters,
+# grid or intervals); the others (uncertainty_samples, interval_method,
+# fit_mode) only steer how a caller serves or refits and may differ
+FIT_FIELDS = ("growth", "n_changepoints", "changepoint_range", "yearly_seasonality",
+              "weekly_seasonality", "daily_seasonality", "seasonality_mode",
+              "seasonality_prior_scale", "holidays_prior_scale", "changepoint_prior_scale",
+              "interval_width")
+
+
+def _fit_fields(cfg: dict) -> dict:
+    base = E.ProphetConfig().__dict__
+    return {k: cfg.get(k, base[k]) for k in FIT_FIELDS}
 
 
 class ParamsStore:
-    """Directory of per-bucket fit records, indexed by integer series keys."""
+    """Directory of per-bucket fit records, indexed by integer series keys.
+
+    Record order (which fit wins for a key that was refitted): records are
+    named ``rec_<generation>_<writer>_<seq>.npz`` and sorted by name.  The
+    default generation is the writer's wall clock (``time.time_ns()``), so
+    with writers on several hosts the rule is only as good as their clock
+    agreement; pass ``generation`` (e.g. a run counter or the training date
+    as an integer) to ``put_batch`` / ``put_record`` when that matters.  Ties
+    of one generation across writers break by writer id.
+
+    Stores written by the first record format (a manifest ``records`` list of
+    ``bucket_NNNNNN.npz`` files, no ``format`` key) open read-compatible:
+    their listed records are indexed first, in manifest order."""
 
     def __init__(self, path: str, config: E.ProphetConfig | None = None, writer: str | None = None):
         self.path = path
@@ -50,7 +76,7 @@ class ParamsStore:
         if os.path.exists(mf):
             with open(mf) as f:
                 self.manifest = json.load(f)
-            if config is not None and E.ProphetConfig(**self.manifest["config"]) != config:
+            if config is not None and _fit_fields(self.manifest["config"]) != _fit_fields(config.__dict__):
                 raise ValueError(f"params store {path!r} holds fits made with a different "
                                  f"ProphetConfig: {self.manifest['config']}")
         else:
@@ -59,6 +85,8 @@ class ParamsStore:
             with open(tmp, "w") as f:
                 json.dump(self.manifest, f, indent=1, default=str)
             os.replace(tmp, mf)
+        # serving-side settings: the caller's, when given (fit fields agree)
+        self._config = config
         self.writer = writer or f"p{os.getpid()}{uuid.uuid4().hex[:8]}"
         self._seq = 0
         self._records = {}
@@ -67,13 +95,34 @@ class ParamsStore:
 
     @property
     def config(self) -> E.ProphetConfig:
-        return E.ProphetConfig(**self.manifest["config"])
+        if self._config is not None:
+            return self._config
+        known = E.ProphetConfig().__dict__
+        return E.ProphetConfig(**{k: v for k, v in self.manifest["config"].items() if k in known})
 
-    def put_batch(self, fb: B.FittedBatch, keys: np.ndarray) -> str:
-        """Persist the fits of one batch; ``keys`` [n, k] integer keys."""
-        return self.put_record(fb.to_record(np.asarray(keys, dtype=np.int64).reshape(fb.n, -1)))
+    @property
+    def legacy_records(self) -> list:
+        """Format-1 record names (manifest order), empty for a format-2 store."""
+        if "format" in self.manifest:
+            return []
+        return list(self.manifest.get("records", []))
 
-    def put_record(self, rec: dict) -> str:
+    def put_batch(self, fb: B.FittedBatch, keys: np.ndarray, metrics: np.ndarray | None = None,
+                  generation: int | None = None) -> str:
+        """Persist the fits of one batch; ``keys`` [n, k] integer keys;
+        ``metrics`` [n, len(CV_METRICS)] the series' cross-validation
+        metrics (what the reference logs per run, 02_training.py:187-192)."""
+        rec = fb.to_record(np.asarray(keys, dtype=np.int64).reshape(fb.n, -1))
+        if metrics is not None:
+            from ._lib import CV_METRICS
+            m = np.asarray(metrics, np.float64)
+            if m.shape != (fb.n, len(CV_METRICS)):
+                raise ValueError(f"metrics must be [{fb.n}, {len(CV_METRICS)}]")
+            rec["cv_metrics"] = m
+            rec["cv_metric_names"] = np.array(CV_METRICS)
+        return self.put_record(rec, generation=generation)
+
+    def put_record(self, rec: dict, generation: int | None = None) -> str:
         """Persist one record (``FittedBatch.to_record`` or
         ``serialize.json_to_record`` fields, with ``keys``).  Raises
         ValueError if the record was fitted under a growth, seasonality mode
@@ -81,7 +130,10 @@ class ParamsStore:
         if "keys" not in rec:
             raise ValueError("record needs integer 'keys' [n, k] to be indexed")
         B.check_record_config(rec, self.config)
-        name = f"{REC_PREFIX}{time.time_ns():020d}_{self.writer}_{self._seq:06d}.npz"
+        gen = time.time_ns() if generation is None else int(generation)
+        if gen < 0:
+            raise ValueError("generation must be >= 0")
+        name = f"{REC_PREFIX}{gen:020d}_{self.writer}_{self._seq:06d}.npz"
         self._seq += 1
         tmp = os.path.join(self.path, f".{name}.{uuid.uuid4().hex}.tmp.npz")
         np.savez(tmp, **rec)
@@ -90,9 +142,10 @@ class ParamsStore:
         return name
 
     def record_names(self) -> list:
-        """Every committed record of every writer, oldest first."""
-        return sorted(f for f in os.listdir(self.path)
-                      if f.startswith(REC_PREFIX) and f.endswith(".npz"))
+        """Every committed record of every writer, oldest first (format-1
+        records first, in their manifest order)."""
+        return self.legacy_records + sorted(
+            f for f in os.listdir(self.path) if f.startswith(REC_PREFIX) and f.endswith(".npz"))
 
     def record(self, name: str) -> dict:
         if name not in self._records:
@@ -112,6 +165,22 @@ class ParamsStore:
             self._index = idx
             self._index_names = names
         return self._index
+
+    def metrics(self, key_cols=("store", "item")) -> pd.DataFrame:
+        """The cross-validation metrics of every indexed series (its winning
+        record), like the per-run metrics MLflow holds for the reference
+        (02_training.py:192): [key_cols..., CV metric columns]; series fitted
+        without ``cv_metrics`` are left out."""
+        rows = {}
+        for k, (name, r) in self.index().items():
+            rec = self.record(name)
+            if "cv_metrics" in rec:
+                rows[k] = (tuple(str(s) for s in rec["cv_metric_names"]), rec["cv_metrics"][r])
+        names = next(iter(rows.values()))[0] if rows else ()
+        out = {c: np.array([k[j] for k in rows], np.int64) for j, c in enumerate(key_cols)}
+        for j, m in enumerate(names):
+            out[m] = np.array([v[1][j] for v in rows.values()], np.float64)
+        return pd.DataFrame(out)
 
     def __len__(self):
         return len(self.index())
@@ -145,68 +214,100 @@ class ForecastStoreItemModel:
         ``model_input``.  Returns [ds, store, item, yhat, yhat_upper,
         yhat_lower]; each group's rows sorted by ds (Prophet.predict order).
         Logistic-growth stores need a ``cap`` column (UPSTREAM predict)."""
+        from .training import dense_frame
         for c in ("ds", "store", "item"):
             if c not in model_input:
                 raise ValueError(f"model_input must have column {c!r}")
         store = self._store
         eng = get_engine(store.config, self._device)
+        dev = torch.device("cuda", eng.device)
         logistic = store.config.growth == "logistic"
         if logistic and "cap" not in model_input:
             raise ValueError('Capacities must be supplied for logistic growth in column "cap"')
         idx = store.index()
-        st_col = model_input["store"].to_numpy(np.int64)
-        it_col = model_input["item"].to_numpy(np.int64)
-        ds_all = B.to_ns(model_input["ds"])
-        cap_all = model_input["cap"].to_numpy(np.float64) if logistic else None
-        n_in = st_col.shape[0]
-        if n_in == 0:
+        cols = ["ds", "store", "item", "yhat", "yhat_upper", "yhat_lower"]
+        if len(model_input) == 0:
             return pd.DataFrame({c: pd.Series(dtype=("datetime64[ns]" if c == "ds" else np.int32
                                                      if c in ("store", "item") else np.float32))
-                                 for c in ["ds", "store", "item", "yhat", "yhat_upper", "yhat_lower"]})
-        # rows ordered by (store, item, ds); an input already in that order
-        # (the usual layout) is not sorted again
-        code = (st_col - int(st_col.min())) * (int(it_col.max()) - int(it_col.min()) + 1) + \
-            (it_col - int(it_col.min()))
-        same = code[1:] == code[:-1]
-        if bool(np.all(code[1:] >= code[:-1])) and bool(np.all(~same | (ds_all[1:] >= ds_all[:-1]))):
-            order = np.arange(n_in)
-            sc = code
-        else:
-            order = np.lexsort((ds_all, code))
-            sc = code[order]
-        brk = np.flatnonzero(sc[1:] != sc[:-1]) + 1
-        starts = np.concatenate(([0], brk))
-        ends = np.concatenate((brk, [len(order)]))
-        # group the groups: same record + same (sorted) dates -> one launch
-        jobs = {}
-        for s, e in zip(starts, ends):
-            key = (int(st_col[order[s]]), int(it_col[order[s]]))
+                                 for c in cols})
+
+        def lookup(key):
             if key not in idx:
                 raise KeyError(f"no fitted model for store={key[0]} item={key[1]} "
                                f"(run_item_{key[1]}_store_{key[0]})")
-            name, row = idx[key]
-            ds = ds_all[order[s:e]]
-            jk = (name, ds.tobytes())
-            jobs.setdefault(jk, (ds, [], [], []))
-            jobs[jk][1].append(row)
-            jobs[jk][2].append(key)
-            if logistic:
-                jobs[jk][3].append(cap_all[order[s:e]])
-        cols = ["ds", "store", "item", "yhat", "yhat_upper", "yhat_lower"]
-        frames = []
-        for (name, _), (ds, rows, keys, caps) in jobs.items():
+            return idx[key]
+
+        # group the groups: same record + same (sorted) dates -> one launch
+        jobs = {}
+        dense = dense_frame(model_input, ["store", "item"], value="cap" if logistic else None)
+        if dense is not None:
+            # grouped input in key order, every group on the same dates: no
+            # per-group date handling (the usual scoring frame)
+            gkeys, ds0, capm = dense
+            for g, key in enumerate(map(tuple, gkeys.tolist())):
+                name, row = lookup(key)
+                j = jobs.setdefault(name, (ds0, [], [], []))
+                j[1].append(row)
+                j[2].append(key)
+                if logistic:
+                    j[3].append(capm[g])
+        else:
+            st_col = model_input["store"].to_numpy(np.int64)
+            it_col = model_input["item"].to_numpy(np.int64)
+            ds_all = B.to_ns(model_input["ds"])
+            cap_all = model_input["cap"].to_numpy(np.float64) if logistic else None
+            n_in = st_col.shape[0]
+            # rows ordered by (store, item, ds); an input already in that
+            # order is not sorted again
+            code = (st_col - int(st_col.min())) * (int(it_col.max()) - int(it_col.min()) + 1) + \
+                (it_col - int(it_col.min()))
+            same = code[1:] == code[:-1]
+            if bool(np.all(code[1:] >= code[:-1])) and bool(np.all(~same | (ds_all[1:] >= ds_all[:-1]))):
+                order = np.arange(n_in)
+                sc = code
+            else:
+                order = np.lexsort((ds_all, code))
+                sc = code[order]
+            brk = np.flatnonzero(sc[1:] != sc[:-1]) + 1
+            starts = np.concatenate(([0], brk))
+            ends = np.concatenate((brk, [len(order)]))
+            for s, e in zip(starts, ends):
+                key = (int(st_col[order[s]]), int(it_col[order[s]]))
+                name, row = lookup(key)
+                ds = ds_all[order[s:e]]
+                j = jobs.setdefault((name, ds.tobytes()), (ds, [], [], []))
+                j[1].append(row)
+                j[2].append(key)
+                if logistic:
+                    j[3].append(cap_all[order[s:e]])
+        # launch every job, D2H into pinned memory asynchronously, then
+        # build the key / date columns while the GPU works
+        launched = []
+        for jk, (ds, rows, keys, caps) in jobs.items():
+            name = jk if isinstance(jk, str) else jk[0]
             fb = B.FittedBatch.from_record(eng, store.record(name), rows)
             Tf, out = fb.predict(ds, seed=self._seed, components=False,
                                  cap=np.stack(caps) if logistic else None)
-            n = len(rows)
+            blk = torch.stack([out[k][:, :Tf] for k in ("yhat", "yhat_upper", "yhat_lower")])
+            host = torch.empty(blk.shape, dtype=blk.dtype, pin_memory=True)
+            host.copy_(blk, non_blocking=True)
+            done = torch.cuda.Event()
+            done.record(torch.cuda.current_stream(dev))
+            launched.append((ds, keys, Tf, host, done))
+        frames = []
+        for ds, keys, Tf, host, done in launched:
+            n = len(keys)
             keys = np.asarray(keys, dtype=np.int64)
-            fr = {"ds": np.tile(ds.astype("datetime64[ns]"), n),
+            fr = {"ds": np.tile(np.asarray(ds, np.int64).view("datetime64[ns]"), n),
                   "store": np.repeat(keys[:, 0].astype(np.int32), Tf),
                   "item": np.repeat(keys[:, 1].astype(np.int32), Tf)}
-            blk = torch.stack([out[k][:, :Tf] for k in ("yhat", "yhat_upper", "yhat_lower")]).cpu().numpy()
+            frames.append((fr, host, done))
+        for fr, host, done in frames:
+            done.synchronize()
+            h = host.numpy()
             for j, k in enumerate(("yhat", "yhat_upper", "yhat_lower")):
-                fr[k] = blk[j].reshape(-1)
-            frames.append(fr)
+                fr[k] = h[j].reshape(-1)
+        frames = [f for f, _, _ in frames]
         return pd.DataFrame({c: (frames[0][c] if len(frames) == 1 else
                                  np.concatenate([f[c] for f in frames])) for c in cols}, copy=False)
 

@@ -147,90 +147,216 @@ def group_frame(df: pd.DataFrame, keys):
     return np.stack([c[first] for c in cols], axis=1), [order[s:e] for s, e in zip(starts, ends)]
 
 
+def dense_frame(df: pd.DataFrame, keys, value: str | None = "y"):
+    """The sales table's usual layout without per-group work: the frame is
+    grouped, its groups come in increasing key order, every group holds the
+    same strictly increasing dates and no ``value`` is NaN.  Returns (group
+    keys [n, k] int64, dates [T] int64 ns, values [n, T] float64 — a view of
+    the ``value`` column, None if ``value`` is None) or None when any of that
+    does not hold (then ``group_frame`` + ``bucket_groups`` run).  Vectorised
+    checks only: O(rows) with no Python loop over groups."""
+    N = len(df)
+    if N == 0 or (value is not None and value not in df):
+        return None
+    cols = [df[k].to_numpy() for k in keys]
+    if any(c.dtype.kind not in "iu" for c in cols):
+        return None
+    ch = cols[0][1:] != cols[0][:-1]
+    for c in cols[1:]:
+        ch |= c[1:] != c[:-1]
+    brk = np.flatnonzero(ch) + 1
+    n = brk.shape[0] + 1
+    T = N // n
+    if T < 2 or n * T != N or (n > 1 and not np.array_equal(brk, np.arange(1, n) * T)):
+        return None
+    gkeys = np.stack([c[::T].astype(np.int64) for c in cols], axis=1)
+    if n > 1:
+        # strictly increasing keys (lexicographic): the general path's group
+        # order, and no key split over two runs
+        inc = np.zeros(n - 1, bool)
+        eq = np.ones(n - 1, bool)
+        for j in range(len(keys)):
+            a = gkeys[:, j]
+            inc |= eq & (a[1:] > a[:-1])
+            eq &= a[1:] == a[:-1]
+        if not bool(inc.all()):
+            return None
+    ds = df["ds"].to_numpy()
+    if ds.dtype.kind != "M":
+        return None
+    if ds.dtype != np.dtype("datetime64[ns]"):
+        ds = ds.astype("datetime64[ns]")
+    dsi = ds.view(np.int64).reshape(n, T)
+    ds0 = dsi[0]
+    if not bool(np.all(ds0[1:] > ds0[:-1])) or (n > 1 and not bool((dsi[1:] == ds0).all())):
+        return None
+    if value is None:
+        return gkeys, np.array(ds0), None
+    y = df[value].to_numpy(np.float64)
+    if bool(np.isnan(y).any()):
+        return None
+    return gkeys, np.array(ds0), y.reshape(n, T)
+
+
+def _empty_frame(cols, keys):
+    return pd.DataFrame({c: pd.Series(dtype=("datetime64[ns]" if c == "ds" else
+                                             np.int32 if c in keys else np.float32))
+                         for c in cols})
+
+
 def forecast_store_items(df: pd.DataFrame, keys=("store", "item"), *, periods: int = HORIZON_DAYS,
                          freq="d", config: E.ProphetConfig | None = None, device=None,
                          seed: int = 0, params_store=None, rank: int = 0,
-                         world_size: int = 1, return_fits: bool = False):
+                         world_size: int = 1, return_fits: bool = False,
+                         cv_metrics: bool = False, return_metrics: bool = False):
     """Batched equivalent of
     ``df.groupBy(*keys).applyInPandas(forecast_store_item, schema)``.
 
     With ``world_size > 1`` only the groups whose splitmix64 key hash maps to
     ``rank`` are processed; ``parallel.gather_frames``
-    collects the per-rank frames."""
+    collects the per-rank frames.
+
+    ``cv_metrics``: the reference's ``train_model`` cross-validation
+    (02_training.py:178-188: horizon 90 days, period 360, initial 730, then
+    ``performance_metrics``) for every series, per bucket on the GPU (fold
+    refits + fold forecasts + K6).  The per-series metrics (the means over
+    horizons of mse, rmse, mae, mape, ... — what :187-192 logs to MLflow) go
+    into each params-store record and, with ``return_metrics``, into a
+    DataFrame [keys..., *CV_METRICS].
+
+    Returns the forecast frame; with ``return_fits`` / ``return_metrics`` a
+    tuple (frame, fits, metrics) holding the requested extras in that order."""
+    from . import diagnostics
+    from . import _lib as L
     keys = list(keys)
     cfg = config or E.ProphetConfig.reference()
     eng = get_engine(cfg, device)
-    gkeys, rows = group_frame(df, keys)
-    if world_size > 1:
-        mine = np.flatnonzero(B.shard_of(gkeys, world_size) == rank)
-        gkeys = gkeys[mine]
-        rows = [rows[i] for i in mine]
-    ds_all = B.to_ns(df["ds"])
-    y_all = df["y"].to_numpy(np.float64)
-    ds_list = [ds_all[r] for r in rows]
-    y_list = [y_all[r] for r in rows]
-    buckets = B.bucket_groups(ds_list, y_list)
-    frames, fits = [], []
+    dev = torch.device("cuda", eng.device)
+    cols = ["ds"] + keys + ["y", "yhat", "yhat_upper", "yhat_lower"]
+    dense = dense_frame(df, keys)
+    if dense is not None:
+        # one bucket, no per-group Python (the sorted sales table)
+        gkeys, ds0, Y = dense
+        if world_size > 1:
+            mine = np.flatnonzero(B.shard_of(gkeys, world_size) == rank)
+            gkeys, Y = gkeys[mine], Y[mine]
+        buckets = [B.Bucket(ds0, ds0, Y, np.arange(gkeys.shape[0]))] if gkeys.shape[0] else []
+        y_list = None
+    else:
+        gkeys, rows = group_frame(df, keys)
+        if world_size > 1:
+            mine = np.flatnonzero(B.shard_of(gkeys, world_size) == rank)
+            gkeys = gkeys[mine]
+            rows = [rows[i] for i in mine]
+        ds_all = B.to_ns(df["ds"])
+        y_all = df["y"].to_numpy(np.float64)
+        ds_list = [ds_all[r] for r in rows]
+        y_list = [y_all[r] for r in rows]
+        buckets = B.bucket_groups(ds_list, y_list)
 
-    def emit(bk, fut, host):
-        # one bucket's rows of the output frame (schema of 02_training.py:307),
-        # as column arrays; the frame is built once at the end
-        bkeys = gkeys[bk.members]
-        Tf = len(fut)
-        n = len(bk.members)
-        yin = np.full((n, Tf), np.nan, np.float32)
-        for i, g in enumerate(bk.members):
-            v = y_list[g]
-            m = min(Tf, len(v))
-            yin[i, :m] = v[:m]
-        fr = {"ds": np.tile(fut.astype("datetime64[ns]"), n)}
-        for j, k in enumerate(keys):
-            fr[k] = np.repeat(bkeys[:, j].astype(np.int32), Tf)
-        fr["y"] = yin.reshape(-1)
-        for k in ("yhat", "yhat_upper", "yhat_lower"):
-            fr[k] = np.ascontiguousarray(host[k][:, :Tf], dtype=np.float32).reshape(-1)
-        frames.append(fr)
-
-    # buckets with compatible layouts (seasonalities, changepoint count) but
-    # different date grids share one ragged launch
+    # phase 1: every launch (fit, forecast, CV folds) and the asynchronous
+    # D2H of each forecast block into pinned memory, so the host assembles
+    # the output columns below while the GPU works
+    launched = []
     for pack in B.ragged_packs(buckets, cfg):
+        bks = [buckets[b] for b in pack]
         if len(pack) == 1:
-            bk = buckets[pack[0]]
+            bk = bks[0]
             bkeys = gkeys[bk.members]
-            fb = B.FittedBatch.fit_dense(eng, bk.fit_ds, bk.Y, history_dates=bk.history_dates,
+            Yd = B._dense(bk.Y, bk.Y.shape[0], bk.Y.shape[1], bk.Y.shape[1], dev) \
+                if cv_metrics else bk.Y
+            fb = B.FittedBatch.fit_dense(eng, bk.fit_ds, Yd, history_dates=bk.history_dates,
                                          series_ids=B.series_id(bkeys))
-            fut = B.future_dates(bk.history_dates, periods, freq, include_history=True)
-            Tf, out = fb.predict(fut, seed=seed, components=False)
-            blk = torch.stack([out[k][:, :Tf] for k in ("yhat", "yhat_upper", "yhat_lower")]).cpu().numpy()
-            emit(bk, fut, {k: blk[j] for j, k in enumerate(("yhat", "yhat_upper", "yhat_lower"))})
-            subs = [(bkeys, fb)]
+            futs = [B.future_dates(bk.history_dates, periods, freq, include_history=True)]
+            Tf, out = fb.predict(futs[0], seed=seed, components=False)
+            blk = torch.stack([out[k][:, :Tf] for k in ("yhat", "yhat_upper", "yhat_lower")])
+            row0 = [0, len(bk.members)]
+            subs = [(bkeys, fb, Yd)]
         else:
-            bks = [buckets[b] for b in pack]
             pkeys = np.concatenate([gkeys[bk.members] for bk in bks])
             rb = B.RaggedFittedBatch.fit_buckets(eng, bks, series_ids=B.series_id(pkeys))
             futs = rb.future(periods, freq)
             _, out = rb.predict(futs, seed=seed, components=False)
-            blk = torch.stack([out[k] for k in ("yhat", "yhat_upper", "yhat_lower")]).cpu().numpy()
-            host = {k: blk[j] for j, k in enumerate(("yhat", "yhat_upper", "yhat_lower"))}
-            subs = []
-            for j, bk in enumerate(bks):
-                r0, r1 = int(rb.row0[j]), int(rb.row0[j + 1])
-                emit(bk, futs[j], {k: v[r0:r1] for k, v in host.items()})
-                subs.append((pkeys[r0:r1], rb.sub_batch(j)))
-        for bkeys, fb in subs:
+            blk = torch.stack([out[k] for k in ("yhat", "yhat_upper", "yhat_lower")])
+            row0 = [int(v) for v in rb.row0]
+            subs = [(pkeys[row0[j]:row0[j + 1]], rb.sub_batch(j), bk.Y) for j, bk in enumerate(bks)]
+        host = torch.empty(blk.shape, dtype=blk.dtype, pin_memory=True)
+        host.copy_(blk, non_blocking=True)
+        done = torch.cuda.Event()
+        done.record(torch.cuda.current_stream(dev))
+        mets = []
+        if cv_metrics:
+            for (bkeys, fb, Yc), bk in zip(subs, bks):
+                mets.append(diagnostics.cv_metrics_device(
+                    eng, bk.fit_ds, Yc, seasons=fb.fit.grid.seasons,
+                    series_ids=B.series_id(bkeys), seed=seed))
+        launched.append((bks, futs, row0, host, done, subs, mets))
+
+    # phase 2: output columns (schema of 02_training.py:307); y is copied by
+    # position from each group's frame (NaN past its rows)
+    frames = []
+    for bks, futs, row0, host, done, subs, mets in launched:
+        for j, bk in enumerate(bks):
+            fut = futs[j]
+            Tf = len(fut)
+            n = len(bk.members)
+            bkeys = gkeys[bk.members]
+            fr = {"ds": np.tile(fut.view("datetime64[ns]"), n)}
+            for c, k in enumerate(keys):
+                fr[k] = np.repeat(bkeys[:, c].astype(np.int32), Tf)
+            yin = np.empty((n, Tf), np.float32)
+            if y_list is None:
+                T = bk.Y.shape[1]
+                m = min(T, Tf)
+                yin[:, :m] = bk.Y[:, :m]
+                yin[:, m:] = np.nan
+            else:
+                yin[:] = np.nan
+                for i, g in enumerate(bk.members):
+                    v = y_list[g]
+                    m = min(Tf, len(v))
+                    yin[i, :m] = v[:m]
+            fr["y"] = yin.reshape(-1)
+            frames.append((fr, host, done, row0[j], row0[j + 1], Tf))
+    outs = []
+    for fr, host, done, r0, r1, Tf in frames:
+        done.synchronize()
+        h = host.numpy()
+        for c, k in enumerate(("yhat", "yhat_upper", "yhat_lower")):
+            v = h[c, r0:r1, :Tf]
+            fr[k] = v.reshape(-1) if v.flags.c_contiguous else np.ascontiguousarray(v).reshape(-1)
+        outs.append(fr)
+
+    # phase 3: params store records (with the CV metrics), extras
+    fits, met_frames = [], []
+    for bks, futs, row0, host, done, subs, mets in launched:
+        for j, (bkeys, fb, _) in enumerate(subs):
+            mh = mets[j].cpu().numpy() if mets else None
             if params_store is not None:
-                params_store.put_batch(fb, bkeys)
+                params_store.put_batch(fb, bkeys, metrics=mh)
             if return_fits:
                 fits.append((bkeys, fb))
-    cols = ["ds"] + keys + ["y", "yhat", "yhat_upper", "yhat_lower"]
-    if frames:
-        res = pd.DataFrame({c: (frames[0][c] if len(frames) == 1 else
-                                np.concatenate([f[c] for f in frames])) for c in cols}, copy=False)
+            if mh is not None:
+                mf = {k: bkeys[:, c].astype(np.int32) for c, k in enumerate(keys)}
+                mf.update({name: mh[:, c] for c, name in enumerate(L.CV_METRICS)})
+                met_frames.append(pd.DataFrame(mf))
+    if outs:
+        res = pd.DataFrame({c: (outs[0][c] if len(outs) == 1 else
+                                np.concatenate([f[c] for f in outs])) for c in cols}, copy=False)
     else:
-        res = pd.DataFrame({c: pd.Series(dtype=("datetime64[ns]" if c == "ds" else
-                                                 np.int32 if c in keys else np.float32))
-                            for c in cols})
-    return (res, fits) if return_fits else res
+        res = _empty_frame(cols, keys)
+    if not (return_fits or return_metrics):
+        return res
+    extra = [res]
+    if return_fits:
+        extra.append(fits)
+    if return_metrics:
+        if not cv_metrics:
+            raise ValueError("return_metrics needs cv_metrics=True")
+        extra.append(pd.concat(met_frames, ignore_index=True) if met_frames else
+                     pd.DataFrame({**{k: pd.Series(dtype=np.int32) for k in keys},
+                                   **{m: pd.Series(dtype=np.float64) for m in L.CV_METRICS}}))
+    return tuple(extra)
 
 
 def forecast_items(df: pd.DataFrame, **kw):

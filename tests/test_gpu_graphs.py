@@ -75,3 +75,32 @@ def test_predict_parts_on_two_streams_equal_one_call(method):
     nc = eng.predict(fit, fg, seed=5, interval_method=method, components=False)
     for k in ("yhat", "yhat_lower", "yhat_upper"):
         assert torch.equal(one[k][:, :fg.T], nc[k][:, :fg.T]), k
+
+
+def test_replay_after_a_larger_fit_on_the_same_engine():
+    """A captured step keeps pointers into its context's fit workspace; a
+    later, larger fit on the engine it was built from (shared per-device
+    context) must not move that workspace under the graph."""
+    ds = synthetic.daily_dates("2016-01-01", "2017-12-31")
+    n = 16
+    Y = synthetic.sales_matrix(n, ds)
+    eng = dfa.Engine(0)
+    st = dfa.ForecastStep(eng, ds, n)
+    assert st.engine.ctx is not eng.ctx
+    st.set_inputs(Y)
+    e = _snap(st.run())
+    st.capture()
+    # a longer grid and a bigger batch on the shared context: its workspace grows
+    big = synthetic.daily_dates()
+    Yb = synthetic.sales_matrix(64, big)
+    seasons = eng.config.seasons(int(big[0]), int(big[-1]), int(big[1] - big[0]))
+    g = dfa.build_grid(big, seasons, start_ns=int(big[0]), t_scale_ns=int(big[-1] - big[0]))
+    Yd = torch.zeros((64, g.T_pad), dtype=torch.float64, device="cuda")
+    Yd[:, :g.T] = torch.from_numpy(Yb).cuda()
+    eng.fit(g, Yd)
+    r = _snap(st.replay())
+    torch.cuda.synchronize()
+    for k in ("theta", "f", "status", "metrics"):
+        assert torch.equal(e[k], r[k]), k
+    for k in ("yhat", "yhat_lower", "yhat_upper"):
+        assert torch.equal(e[k][:, :st.Tf], r[k][:, :st.Tf]), k

@@ -730,3 +730,44 @@ def test_cv_metrics_single_group_insample(eng, n):
         for j, k in enumerate(L.CV_METRICS):
             want = float(np.mean(pm[k]))
             assert abs(m[s, j] - want) <= 1e-12 * max(1.0, abs(want)), (n, s, k, m[s, j], want)
+
+
+def test_forecast_store_items_cv_metrics(eng, golden_ref, tmp_path):
+    """The reference's train_model always cross-validates (02_training.py:
+    178-188).  forecast_store_items(cv_metrics=True) computes the same
+    per-series metrics on the batched path: equal to the per-group
+    train_model(cv_metrics=True) values, to the oracle's performance_metrics
+    means (golden fixture) within 1e-4, persisted in the params store, and
+    the forecast rows unchanged by the CV work."""
+    import pandas as pd
+    ds, Y = golden_ref["ds_ns"], golden_ref["Y"][:2]
+    T = len(ds)
+    df = pd.DataFrame({"ds": np.tile(ds.view("datetime64[ns]"), 2),
+                       "store": np.repeat(np.int32([3, 3]), T),
+                       "item": np.repeat(np.int32([1, 2]), T), "y": Y.reshape(-1)})
+    store = dfa.ParamsStore(str(tmp_path / "p"))
+    res, met = dfa.forecast_store_items(df, cv_metrics=True, return_metrics=True,
+                                        params_store=store)
+    plain = dfa.forecast_store_items(df)
+    assert res.equals(plain)
+    assert list(met.columns) == ["store", "item"] + list(dfa.CV_METRICS)
+    assert met[["store", "item"]].to_numpy().tolist() == [[3, 1], [3, 2]]
+    names = list(golden_ref["cv_metric_names"])
+    for j, k in enumerate(names):
+        got, want = met[k].to_numpy(), golden_ref["cv_metrics"][:, j]
+        assert np.all(np.abs(got - want) <= 1e-4 * np.abs(want)), (k, got, want)
+    for i in range(2):
+        one = df[df.item == i + 1].reset_index(drop=True)
+        m = dfa.train_model(one, store=3, cv_metrics=True).metrics
+        for k in dfa.CV_METRICS[:5]:
+            assert abs(m[k] - met[k].iloc[i]) <= 1e-9 * abs(m[k]), (k, m[k], met[k].iloc[i])
+    sm = store.metrics()
+    assert np.allclose(sm[list(dfa.CV_METRICS[:5])].to_numpy(), met[list(dfa.CV_METRICS[:5])].to_numpy(),
+                       rtol=0, atol=0)
+    # ragged frames (per-bucket CV inside a ragged pack) give each bucket's metrics
+    stag = synthetic.staggered_frame(1, 6, n_starts=3, n_ends=1, max_delay_days=200)
+    r2, m2 = dfa.forecast_store_items(stag, cv_metrics=True, return_metrics=True)
+    assert len(m2) == 6 and np.isfinite(m2["mse"]).all()
+    g = stag[stag.item == 4].reset_index(drop=True)
+    m1 = dfa.train_model(g, store=1, cv_metrics=True).metrics
+    assert abs(m1["mse"] - m2[m2.item == 4]["mse"].iloc[0]) <= 1e-9 * m1["mse"]

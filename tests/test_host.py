@@ -375,3 +375,103 @@ def test_group_frame_and_buckets_fast_paths():
     mixed = B.bucket_groups([ds[r] for r in r0], yn)
     assert len(mixed) == 2 and sorted(len(b.members) for b in mixed) == [1, 11]
     assert pd.Series([b.fit_ds.shape[0] for b in mixed]).isin([90, 91]).all()
+
+
+# ------------------------------------------------------ round-3 host additions
+def test_dense_frame_fast_path_agrees_with_general_path():
+    """training.dense_frame (the sorted sales table: no per-group work) gives
+    the groups, dates and values group_frame + bucket_groups give, and
+    declines every layout it does not cover."""
+    df = synthetic.store_item_frame(3, 4, "2016-01-01", "2017-12-31")
+    gk, ds0, Y = training.dense_frame(df, ["store", "item"])
+    g1, rows = training.group_frame(df, ["store", "item"])
+    ds = B.to_ns(df["ds"])
+    y = df["y"].to_numpy(np.float64)
+    bks = B.bucket_groups([ds[r] for r in rows], [y[r] for r in rows])
+    assert len(bks) == 1 and np.array_equal(gk, g1)
+    assert np.array_equal(ds0, bks[0].fit_ds) and np.array_equal(Y, bks[0].Y)
+    assert np.shares_memory(Y, df["y"].to_numpy())          # a view, no copy
+    _, _, none = training.dense_frame(df, ["store", "item"], value=None)
+    assert none is None
+    # declined: NaN y, shuffled groups, unequal lengths, different dates, unsorted dates
+    d = df.copy()
+    d.loc[5, "y"] = np.nan
+    assert training.dense_frame(d, ["store", "item"]) is None
+    assert training.dense_frame(df.iloc[::-1].reset_index(drop=True), ["store", "item"]) is None
+    order = np.concatenate([np.arange(731, 2 * 731), np.arange(731), np.arange(2 * 731, len(df))])
+    assert training.dense_frame(df.iloc[order].reset_index(drop=True), ["store", "item"]) is None
+    assert training.dense_frame(df.iloc[1:].reset_index(drop=True), ["store", "item"]) is None
+    d = df.copy()
+    d.loc[731, "ds"] = d.loc[731, "ds"] - pd.Timedelta(days=1)
+    assert training.dense_frame(d, ["store", "item"]) is None
+    assert training.dense_frame(df.iloc[:0], ["store", "item"]) is None
+
+
+def _legacy_store(path, recs):
+    """A params store in the first record format (manifest 'records' list of
+    bucket_NNNNNN.npz files, no 'format' key)."""
+    import json
+    import os
+    os.makedirs(path, exist_ok=True)
+    names = []
+    for i, rec in enumerate(recs):
+        name = f"bucket_{i:06d}.npz"
+        np.savez(os.path.join(path, name), **rec)
+        names.append(name)
+    with open(os.path.join(path, "manifest.json"), "w") as f:
+        json.dump({"records": names, "config": ProphetConfig.reference().__dict__}, f)
+
+
+def test_params_store_reads_format_1(tmp_path):
+    """a store written by the previous code is indexed (its listed
+    bucket records first, in manifest order), not silently empty; new records
+    of the current format win for refitted keys."""
+    from distributed_forecasting_amd import serialize
+    r1 = serialize.json_to_record(_json_model("multiplicative"), keys=[1, 2])
+    r2 = serialize.json_to_record(_json_model("multiplicative"), keys=[1, 3])
+    r3 = dict(r1, keys=np.array([[1, 2]], np.int64))        # refit of (1, 2) in the old store
+    path = str(tmp_path / "old")
+    _legacy_store(path, [r1, r2, r3])
+    st = dfa.ParamsStore(path)
+    assert st.legacy_records == ["bucket_000000.npz", "bucket_000001.npz", "bucket_000002.npz"]
+    idx = st.index()
+    assert idx[(1, 2)] == ("bucket_000002.npz", 0) and idx[(1, 3)] == ("bucket_000001.npz", 0)
+    name = st.put_record(dict(r2))
+    assert st.index()[(1, 3)] == (name, 0) and len(st) == 2
+
+
+def test_params_store_serving_fields_may_differ(tmp_path):
+    """reopening a store with other serving-only settings
+    (uncertainty_samples, interval_method, fit_mode) is allowed and those
+    settings are the caller's; fit-defining fields must agree."""
+    from dataclasses import replace
+    path = str(tmp_path / "s")
+    dfa.ParamsStore(path)
+    cfg = replace(ProphetConfig.reference(), uncertainty_samples=200, interval_method="sample",
+                  fit_mode="stan")
+    st = dfa.ParamsStore(path, config=cfg)
+    assert st.config.uncertainty_samples == 200 and st.config.fit_mode == "stan"
+    with pytest.raises(ValueError, match="different ProphetConfig"):
+        dfa.ParamsStore(path, config=replace(ProphetConfig.reference(), changepoint_prior_scale=0.5))
+    with pytest.raises(ValueError, match="different ProphetConfig"):
+        dfa.ParamsStore(path, config=replace(ProphetConfig.reference(), n_changepoints=10))
+
+
+def test_params_store_generation_and_metrics(tmp_path):
+    """A caller-given generation orders refits independently of wall clocks;
+    metrics() returns the winning record's CV metrics per key."""
+    from distributed_forecasting_amd import serialize
+    st = dfa.ParamsStore(str(tmp_path / "s"), writer="a")
+    other = dfa.ParamsStore(str(tmp_path / "s"), writer="b")
+    rec = serialize.json_to_record(_json_model("multiplicative"), keys=[4, 5])
+    m_new = np.arange(len(dfa.CV_METRICS), dtype=np.float64)[None, :]
+    newer = dict(rec, cv_metrics=m_new, cv_metric_names=np.array(dfa.CV_METRICS))
+    older = dict(rec, cv_metrics=m_new + 100, cv_metric_names=np.array(dfa.CV_METRICS))
+    n2 = other.put_record(newer, generation=2)
+    st.put_record(older, generation=1)                        # written later, older generation
+    assert st.index()[(4, 5)] == (n2, 0)
+    met = st.metrics()
+    assert list(met.columns) == ["store", "item"] + list(dfa.CV_METRICS)
+    assert met.shape[0] == 1 and met["mse"].iloc[0] == 0.0 and met["mdape"].iloc[0] == 6.0
+    with pytest.raises(ValueError):
+        st.put_record(rec, generation=-1)
