@@ -38,6 +38,7 @@ struct pf_timed {
 
 struct pf_ctx {
   int device;
+  int n_cu;         // compute units of the device (persistent K3T grid)
   char err[512];
   void *ws;         // scratch owned by the context (lane-blocked grid copy)
   size_t ws_bytes;
@@ -427,6 +428,7 @@ struct FitKArgs {
   // (32 or 48), features >= K zero (NULL unless the tiled path may run)
   const double *XR;
   int XR_width;
+  int *queue;                // K3T work-queue counter (context scratch)
   const double *sigmas, *s_a, *s_m;
   double tau;
   // hyperparameter batching: per-series prior scales (NULL: the shared
@@ -2047,11 +2049,13 @@ int pf_ctx_create(int device, pf_ctx **out) {
   c->n_timed = 0;
   c->n_events = 0;
   hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device);
   if (e != hipSuccess) {
     snprintf(g_err_noctx, sizeof g_err_noctx, "hipSetDevice(%d): %s", device, hipGetErrorString(e));
     delete c;
     return -2;
   }
+  if (c->n_cu < 1) c->n_cu = 256;
   *out = c;
   return 0;
 }
@@ -2432,8 +2436,12 @@ int launch_fitlike(pf_ctx *ctx, int what, const FitKArgs &a, int n, hipStream_t 
           auto kt = k_fit_tile<MODE, TKP>;
           PF_HIP(ctx, hipFuncSetAttribute((const void *)kt, hipFuncAttributeMaxDynamicSharedMemorySize,
                                           (int)smem_t));
+          // persistent tiles: one workgroup per CU (the LDS budget), series
+          // handed out by the queue counter after the first 16 per tile
           const int nt = (n + PF_TS - 1) / PF_TS;
-          PF_TIMED_LAUNCH(ctx, "k_fit_tile", nt, st, kt, dim3(nt), dim3(PF_TNW * 64), smem_t, st, b, n);
+          const int grid = nt < ctx->n_cu ? nt : ctx->n_cu;
+          PF_HIP(ctx, hipMemsetD32Async((hipDeviceptr_t)b.queue, grid * PF_TS, 1, st));
+          PF_TIMED_LAUNCH(ctx, "k_fit_tile", grid, st, kt, dim3(grid), dim3(PF_TNW * 64), smem_t, st, b, n);
         }
       } else {
         PF_TIMED_LAUNCH(ctx, v ? "k_fit_resume" : "k_fit", n, st, kf[v], dim3(n), dim3(NW * 64),
@@ -2530,7 +2538,7 @@ static int prepare_fit_scratch(pf_ctx *ctx, FitKArgs &a, hipStream_t st, bool ro
     return 0;
   }
   const int W = a.K <= 32 ? 32 : 48;
-  const size_t rbytes = rowmajor ? (size_t)a.Tp * W * sizeof(double) : 0;
+  const size_t rbytes = rowmajor ? (size_t)a.Tp * W * sizeof(double) + 256 : 0;
   void *w = nullptr;
   const int rc = ctx_workspace(ctx, gbytes + rbytes, &w);
   if (rc) return rc;
@@ -2554,6 +2562,7 @@ static int prepare_fit_scratch(pf_ctx *ctx, FitKArgs &a, hipStream_t st, bool ro
     PF_HIP(ctx, hipGetLastError());
     a.XR = xr;
     a.XR_width = W;
+    a.queue = (int *)((char *)xr + (size_t)a.Tp * W * sizeof(double));
   }
   return 0;
 }

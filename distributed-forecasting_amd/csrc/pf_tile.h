@@ -93,12 +93,13 @@ struct TileSmem {
   TileZ *z;                      // [16]
   int *flag;                     // [4]
   int *wseg;                     // [2][4] first / last segment of each wave's rows
+  int *sidx;                     // [16] series of each slot (-1: retired)
   static constexpr size_t bytes() {
     const size_t vec = (size_t)PF_TS * TV;
     const size_t d = (1 + 2 * PF_TH) * vec + PF_TS * PF_TH + 2 * PF_TS * PF_TSEG +
                      (Tr::HA ? 2 : 1) * KP * PF_TS + 2 * Tr::NSET * KP * PF_TS +
                      2 * PF_TSLOT * PF_TS + 4 * PF_TS + 2 * PF_TS + 4 * 64;
-    return d * sizeof(double) + PF_TS * sizeof(TileZ) + 4 * sizeof(int) + 8 * sizeof(int) + 64;
+    return d * sizeof(double) + PF_TS * sizeof(TileZ) + (4 + 8 + PF_TS) * sizeof(int) + 64;
   }
   __device__ void carve(char *base) {
     double *p = reinterpret_cast<double *>(base);
@@ -124,6 +125,7 @@ struct TileSmem {
     z = reinterpret_cast<TileZ *>(p);
     flag = reinterpret_cast<int *>(z + PF_TS);
     wseg = flag + 4;
+    sidx = wseg + 8;
   }
 };
 
@@ -290,15 +292,15 @@ struct TileIn {
 // (gb slot w & 1 — waves 2, 3 add onto waves 0, 1 after a barrier —, sg0/sg1
 // at segment + wave, rr[wave]); the segment slots were zeroed by the caller.
 template <int MODE, int KP>
-__device__ __forceinline__ void tile_rows(const FitKArgs &a, TileSmem<MODE, KP> &sm, int tile, int n) {
+__device__ __forceinline__ void tile_rows(const FitKArgs &a, TileSmem<MODE, KP> &sm) {
   using Tr = TileTr<MODE, KP>;
   constexpr int NSET = Tr::NSET, NKS = Tr::NKS, NFT = Tr::NFT;
   constexpr bool HM = Tr::HM, HA = Tr::HA, LOGI = Tr::LOGI;
   const int lane = pf_lane(), wave = __builtin_amdgcn_readfirstlane(pf_wave());
   const int T = a.T, Tp = a.Tp;
   const int j = lane & 15, rq = lane >> 4;
-  const int s_g = tile * PF_TS + j;
-  const bool svalid = s_g < n;
+  const int s_g = sm.sidx[j];          // this slot's series (-1: empty slot)
+  const bool svalid = s_g >= 0;
   const double *kseg = sm.kseg + j * PF_TSEG, *mseg = sm.mseg + j * PF_TSEG;
   const int jrow = 4 * (j & 3) + (j >> 2);
   // feature of Xb k-step kk at lane k index rq
@@ -314,22 +316,20 @@ __device__ __forceinline__ void tile_rows(const FitKArgs &a, TileSmem<MODE, KP> 
   // unconditional (T_pad % 128 == 0 keeps every chunk row in range, XR is
   // zero past K, rows of series past n read 0 from the y buffer's range
   // check), so no predicated load drains the prefetch.
-  const int nvalid = min(n - tile * PF_TS, PF_TS);
   const __amdgpu_buffer_rsrc_t rXR = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<double *>(a.XR), (short)0, Tp * KP * 8, 0x00020000);
   const __amdgpu_buffer_rsrc_t rT = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<double *>(a.t), (short)0, Tp * 8, 0x00020000);
   const __amdgpu_buffer_rsrc_t rS = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<int32_t *>(a.seg), (short)0, Tp * 4, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rY = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<double *>(a.y_scaled + (size_t)tile * PF_TS * Tp), (short)0, nvalid * Tp * 8,
-      0x00020000);
-  const __amdgpu_buffer_rsrc_t rC = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<double *>(LOGI ? a.cap_scaled + (size_t)tile * PF_TS * Tp : a.y_scaled), (short)0,
-      nvalid * Tp * 8, 0x00020000);
+  // y / cap rows of the slot's series (any series of the batch: 64-bit
+  // per-lane bases; an empty slot reads series 0 and masks it)
+  const size_t srow = (size_t)(svalid ? s_g : 0) * Tp + 4 * rq;
+  const pf_d2 *yb = reinterpret_cast<const pf_d2 *>(a.y_scaled + srow);
+  const pf_d2 *cb = reinterpret_cast<const pf_d2 *>((LOGI ? a.cap_scaled : a.y_scaled) + srow);
   const int oxa = (jrow * KP + 8 * rq) * 8, oxa2 = (jrow * KP + 32 + 4 * rq) * 8;
   const int oxg = (4 * rq * KP + 2 * j) * 8, oxg2 = (4 * rq * KP + 32 + j) * 8;
-  const int ot = 4 * rq * 8, oy = (j * Tp + 4 * rq) * 8, os = 4 * rq * 4;
+  const int ot = 4 * rq * 8, os = 4 * rq * 4;
   auto ld2 = [](__amdgpu_buffer_rsrc_t r, int vo, int so) {
     return __builtin_bit_cast(pf_d2, __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, 0));
   };
@@ -351,11 +351,11 @@ __device__ __forceinline__ void tile_rows(const FitKArgs &a, TileSmem<MODE, KP> 
     }
     in.t[0] = ld2(rT, ot, r0 * 8);
     in.t[1] = ld2(rT, ot + 16, r0 * 8);
-    in.y[0] = ld2(rY, oy, r0 * 8);
-    in.y[1] = ld2(rY, oy + 16, r0 * 8);
+    in.y[0] = yb[r0 / 2];
+    in.y[1] = yb[r0 / 2 + 1];
     if constexpr (LOGI) {
-      in.cp[0] = ld2(rC, oy, r0 * 8);
-      in.cp[1] = ld2(rC, oy + 16, r0 * 8);
+      in.cp[0] = cb[r0 / 2];
+      in.cp[1] = cb[r0 / 2 + 1];
     }
     in.sg = __builtin_bit_cast(pf_i4, __builtin_amdgcn_raw_buffer_load_b128(rS, os, r0 * 4, 0));
   };
@@ -935,23 +935,70 @@ __device__ __forceinline__ bool tile_lbfgs(const pf_fit_opts &o, TileSmem<MODE, 
   return need;
 }
 
-// K3T kernel: grid = ceil(n / 16) tiles.  Pass-0 semantics of fit_body
-// (theta in: init; out: the L-BFGS endpoint, f, f_stan, status, n_iter,
-// n_eval); warm = the iteration cap is the warm-up cap (MAXIT -> WARMUP).
+// Load series idx into slot j (the 16 lanes of the slot's group): theta0
+// into the registers and the LDS trial point, a fresh L-BFGS state.  Returns
+// false for a constant series (outputs written here: the optimizer is
+// skipped, Prophet's rule).
+template <int MODE, int KP>
+__device__ __forceinline__ bool tile_load_series(const FitKArgs &a, TileSmem<MODE, KP> &sm, int j, int g,
+                                                 int idx, TileZ &zl, TVec<TileTr<MODE, KP>::NP> &xk,
+                                                 TVec<TileTr<MODE, KP>::NP> &gk,
+                                                 TVec<TileTr<MODE, KP>::NP> &pk,
+                                                 TVec<TileTr<MODE, KP>::NP> &gq) {
+  using Tr = TileTr<MODE, KP>;
+  const int P = a.P, S = a.S;
+  double *xq = sm.xq + (size_t)j * Tr::TV;
+  double *th = a.theta + (size_t)idx * P;
+#pragma unroll
+  for (int i = 0; i < Tr::NP; ++i) {
+    const int p = g + 16 * i;
+    const double v = (p < P) ? th[p] : 0.0;
+    if (p < Tr::TV) xq[p] = v;
+    xk[i] = v;
+    gk[i] = 0.0;
+    pk[i] = 0.0;
+    gq[i] = 0.0;
+  }
+  memset(&zl, 0, sizeof(TileZ));
+  zl.state = LB_INIT;
+  if (a.status[idx] == PF_ST_CONSTANT) {
+    if (g == 0) {
+      th[2 + S] = log(1e-9);
+      a.f_out[idx] = NAN;
+      a.f_stan[idx] = NAN;
+      a.n_iter[idx] = 0;
+      a.n_eval[idx] = 0;
+    }
+    zl.done = 1;
+    return false;
+  }
+  return true;
+}
+
+// K3T kernel, persistent: grid = min(tiles, CUs) workgroups of 16 series
+// slots.  Slot j of workgroup b starts on series 16 b + j; a slot whose
+// series terminates writes that series' outputs and takes the next series
+// from the batch's work queue (a global counter, one atomic per refill), so
+// a tile no longer waits for the slowest of 16 fixed series — it runs until
+// the queue is empty and its last series have finished.  A series computes
+// the same arithmetic in any slot (the MFMA columns, segment slots and DPP
+// rows are per series), so results do not depend on the schedule.
+// Pass-0 semantics of fit_body (theta in: init; out: the L-BFGS endpoint,
+// f, f_stan, status, n_iter, n_eval); warm = the iteration cap is the
+// warm-up cap (MAXIT -> WARMUP).
 // Per evaluation: row pass (all waves; one internal barrier) | barrier |
 // assemble (16 lanes per series) | barrier | zero segment slots + L-BFGS
-// step + publish | barrier.
+// step (+ outputs and refill) + publish | barrier.
 template <int MODE, int KP>
 __global__ __launch_bounds__(PF_TNW * 64, 1) void k_fit_tile(FitKArgs a, int n) {
   using Tr = TileTr<MODE, KP>;
-  constexpr int NP = Tr::NP, TV = Tr::TV;
+  constexpr int NP = Tr::NP;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   TileSmem<MODE, KP> sm;
   sm.carve(smem_raw);
-  const int tile = blockIdx.x, lane = pf_lane(), wave = __builtin_amdgcn_readfirstlane(pf_wave());
+  const int lane = pf_lane(), wave = __builtin_amdgcn_readfirstlane(pf_wave());
   const int P = a.P, S = a.S, T = a.T;
-  const int j = (4 * wave + (lane >> 4)) & 15, g = lane & 15;  // series j's 16 lanes
-  const int sgl = tile * PF_TS + j;
+  const int j = (4 * wave + (lane >> 4)) & 15, g = lane & 15;  // slot j's 16 lanes
   const bool warm = a.warm_cap != 0;
   const pf_fit_opts o = a.o;
   if (threadIdx.x < 64) {
@@ -976,32 +1023,48 @@ __global__ __launch_bounds__(PF_TNW * 64, 1) void k_fit_tile(FitKArgs a, int n) 
   }
   for (int e = threadIdx.x; e < 2 * PF_TSLOT * PF_TS; e += PF_TNW * 64) sm.sg0[e] = 0.0;
   TVec<NP> xk, gk, pk, gq;
-  {
-    TileZ &z = sm.z[j];
-    const bool live = sgl < n && a.status[sgl] != PF_ST_CONSTANT;
-    double *xq = sm.xq + (size_t)j * TV;
-#pragma unroll
-    for (int i = 0; i < NP; ++i) {
-      const int p = g + 16 * i;
-      const double v = (sgl < n && p < P) ? a.theta[(size_t)sgl * P + p] : 0.0;
-      if (p < TV) xq[p] = v;
-      xk[i] = v;
-      gk[i] = 0.0;
-      pk[i] = 0.0;
-      gq[i] = 0.0;
+  // take series from the queue until one needs fitting (or the queue is
+  // empty: the slot retires with sidx = -1); group-uniform loop
+  auto refill = [&](TileZ &zl, int first) {
+    int idx = first;
+    while (true) {
+      if (idx < 0) {
+        int t = 0;
+        if (g == 0) t = atomicAdd(a.queue, 1);
+        idx = dpp_i32<PF_DPP_ROWBCAST(0)>(t);
+      }
+      if (idx >= n) {
+        memset(&zl, 0, sizeof(TileZ));
+        zl.done = 1;
+        return -1;
+      }
+      if (tile_load_series<MODE, KP>(a, sm, j, g, idx, zl, xk, gk, pk, gq)) return idx;
+      idx = -1;
     }
+  };
+  int sidx;
+  {
+    TileZ zl;
+    sidx = refill(zl, (int)blockIdx.x * PF_TS + j);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     if (g == 0) {
-      memset(&z, 0, sizeof(TileZ));
-      z.state = LB_INIT;
-      z.done = live ? 0 : 1;
+      sm.z[j] = zl;
+      sm.sidx[j] = sidx;
     }
   }
   __syncthreads();
-  tile_publish<MODE, KP>(a, sm, j, g);
+  if (sidx >= 0) tile_publish<MODE, KP>(a, sm, j, g);
   __syncthreads();
+  {
+    const unsigned long long any = __ballot(sidx >= 0);
+    if (lane == 0) sm.flag[wave] = any != 0ull ? 1 : 0;
+  }
+  __syncthreads();
+  if (!__builtin_amdgcn_readfirstlane(sm.flag[0] | sm.flag[1] | sm.flag[2] | sm.flag[3])) return;
   while (true) {
     PF_STAMP(0);
-    tile_rows<MODE, KP>(a, sm, tile, n);
+    tile_rows<MODE, KP>(a, sm);
     PF_STAMP(1);
     __syncthreads();
     PF_STAMP(2);
@@ -1021,12 +1084,34 @@ __global__ __launch_bounds__(PF_TNW * 64, 1) void k_fit_tile(FitKArgs a, int n) 
         zl.bad = bad ? 1 : 0;
         zl.n_eval++;
         need = tile_lbfgs<MODE, KP>(o, sm, zl, j, g, P, xk, gk, pk, gq);
-        if (!need) zl.done = 1;
+        if (!need) {
+          // series finished: its outputs, then the slot's next series
+          double *th = a.theta + (size_t)sidx * P;
+#pragma unroll
+          for (int i = 0; i < NP; ++i) {
+            const int p = g + 16 * i;
+            if (p < P) th[p] = xk[i];
+          }
+          if (g == 0) {
+            int st = zl.ret;
+            if (warm && st == PF_ST_MAXIT) st = PF_ST_WARMUP;
+            a.f_out[sidx] = zl.fk;
+            a.f_stan[sidx] = zl.fk;
+            a.n_iter[sidx] = zl.itNum;
+            a.n_eval[sidx] = zl.n_eval;
+            a.status[sidx] = st;
+          }
+          sidx = refill(zl, -1);
+          need = sidx >= 0;
+        }
       }
       PF_STAMP(4);
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
-      if (g == 0) z = zl;
+      if (g == 0) {
+        z = zl;
+        sm.sidx[j] = sidx;
+      }
       if (need) tile_publish<MODE, KP>(a, sm, j, g);
       const unsigned long long any = __ballot(need);
       if (lane == 0) sm.flag[wave] = any != 0ull ? 1 : 0;
@@ -1036,35 +1121,5 @@ __global__ __launch_bounds__(PF_TNW * 64, 1) void k_fit_tile(FitKArgs a, int n) 
     PF_STAMP(6);
     const int more = sm.flag[0] | sm.flag[1] | sm.flag[2] | sm.flag[3];
     if (!__builtin_amdgcn_readfirstlane(more)) break;
-  }
-  // outputs (pass-0 semantics of fit_body)
-  if (sgl < n) {
-    const TileZ &z = sm.z[j];
-    double *th = a.theta + (size_t)sgl * P;
-    const int st_in = a.status[sgl];
-    if (st_in == PF_ST_CONSTANT) {
-      if (g == 0) {
-        th[2 + S] = log(1e-9);
-        a.f_out[sgl] = NAN;
-        a.f_stan[sgl] = NAN;
-        a.n_iter[sgl] = 0;
-        a.n_eval[sgl] = 0;
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < NP; ++i) {
-        const int p = g + 16 * i;
-        if (p < P) th[p] = xk[i];
-      }
-      if (g == 0) {
-        int st = z.ret;
-        if (warm && st == PF_ST_MAXIT) st = PF_ST_WARMUP;
-        a.f_out[sgl] = z.fk;
-        a.f_stan[sgl] = z.fk;
-        a.n_iter[sgl] = z.itNum;
-        a.n_eval[sgl] = z.n_eval;
-        a.status[sgl] = st;
-      }
-    }
   }
 }
