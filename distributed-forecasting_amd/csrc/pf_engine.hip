@@ -1960,7 +1960,9 @@ __device__ __forceinline__ void pred_row_dot(const PredKArgs &a, const PredSerie
 // the interval endpoints of deterministic rows are exact order-statistic
 // draws (pf_ostat.h); rows left to k_predict_mc are not written here.
 __device__ __forceinline__ void det_row(const PredKArgs &a, const PredSeries &ps, int series,
-                                        uint32_t sid, int row, double t_max) {
+                                        uint32_t sid, int row, double t_max,
+                                        const int *__restrict__ comp_col0,
+                                        const int *__restrict__ comp_ncol) {
   const double ysc = ps.ysc;
   const double ti = a.t[row];
   const int sg = a.seg[row];
@@ -1971,7 +1973,7 @@ __device__ __forceinline__ void det_row(const PredKArgs &a, const PredSeries &ps
     // predict_seasonal_components, MAP: the mean); additive parts x y_scale
     for (int b = 0; b < a.n_comp; ++b) {
       double cb = 0.0;
-      const int c0 = a.comp_col0[b], c1 = c0 + a.comp_ncol[b];
+      const int c0 = comp_col0[b], c1 = c0 + comp_ncol[b];
       for (int f = c0; f < c1; ++f) {
         const double xv = a.XT[(size_t)f * a.Tp + row];
         cb += xv * ps.bm[f] + xv * ps.ba[f] * ysc;
@@ -2014,6 +2016,10 @@ __device__ __forceinline__ void det_row(const PredKArgs &a, const PredSeries &ps
 // PF_DET_RPT rows per thread (strided by the block): the per-series setup is
 // paid once per 256 * PF_DET_RPT rows
 #define PF_DET_RPT 4
+// The component column table is indexed at run time: it is read from the
+// kernel argument block (a0), never from the thread's copy `a` (a dynamically
+// indexed local array lives in scratch: the whole argument struct was
+// written to scratch by every thread — 5x the kernel's output bytes).
 template <int KMAX>
 __global__ __launch_bounds__(256) void k_predict_det(PredKArgs a0) {
   __shared__ PredSeries ps;
@@ -2027,7 +2033,7 @@ __global__ __launch_bounds__(256) void k_predict_det(PredKArgs a0) {
 #pragma unroll 1
   for (int r = 0; r < PF_DET_RPT; ++r) {
     const int row = (blockIdx.x * PF_DET_RPT + r) * 256 + threadIdx.x;
-    if (row < a.Tf) det_row(a, ps, series, sid, row, t_max);
+    if (row < a.Tf) det_row(a, ps, series, sid, row, t_max, a0.comp_col0, a0.comp_ncol);
   }
 }
 

@@ -29,11 +29,13 @@
 // elementwise VALU work, and global loads run two chunks ahead (one wave per
 // SIMD: nothing else hides L2 / HBM latency).
 //
-// Reproducibility: no floating-point atomics.  Segment sums go to per-wave
-// slots (wave w writes segment s at slot s + w; the waves' segment ranges
-// are contiguous and ordered, so the slots are disjoint), the beta gradient
-// and residual sums to per-wave slots, and the assemble step adds them in a
-// fixed order — a tile's iterates are bitwise identical run to run.
+// Reproducibility: every LDS accumulator has exactly one writer wave.
+// Segment sums go to per-wave slots (wave w adds segment s at slot s + w;
+// the waves' segment ranges are contiguous and ordered, so the slots are
+// disjoint) — LDS adds of one wave to its own addresses apply in program
+// order —, the beta gradient and residual sums to per-wave slots, and the
+// assemble step adds the slots in a fixed order: a tile's iterates are
+// bitwise identical run to run.
 //
 // L-BFGS: every series owns 16 lanes (4 series per wave, all 4 waves busy)
 // running Stan 2.19's BFGSMinimizer<LBFGSUpdate> + Wolfe line search (same
@@ -85,7 +87,7 @@ struct TileSmem {
   double *hrho;                  // [16][H]
   double *kseg, *mseg;           // [16][PF_TSEG]
   double *bm, *ba;               // [KP][16] (ba only with additive terms)
-  double *gb;                    // [2 slots][NSET][KP][16] beta-gradient partials
+  double *gb;                    // [4 waves][NSET][KP][16] beta-gradient partials
   double *sg0, *sg1;             // [PF_TSLOT][16] per-wave segment-sum slots
   double *rr;                    // [4 waves][16]
   double *sig;                   // [16][2] sigma, 1/sigma^2
@@ -97,7 +99,7 @@ struct TileSmem {
   static constexpr size_t bytes() {
     const size_t vec = (size_t)PF_TS * TV;
     const size_t d = (1 + 2 * PF_TH) * vec + PF_TS * PF_TH + 2 * PF_TS * PF_TSEG +
-                     (Tr::HA ? 2 : 1) * KP * PF_TS + 2 * Tr::NSET * KP * PF_TS +
+                     (Tr::HA ? 2 : 1) * KP * PF_TS + 4 * Tr::NSET * KP * PF_TS +
                      2 * PF_TSLOT * PF_TS + 4 * PF_TS + 2 * PF_TS + 4 * 64;
     return d * sizeof(double) + PF_TS * sizeof(TileZ) + (4 + 8 + PF_TS) * sizeof(int) + 64;
   }
@@ -113,7 +115,7 @@ struct TileSmem {
     bm = p; p += KP * PF_TS;
     ba = Tr::HA ? p : bm;
     if (Tr::HA) p += KP * PF_TS;
-    gb = p; p += 2 * Tr::NSET * KP * PF_TS;
+    gb = p; p += 4 * Tr::NSET * KP * PF_TS;
     sg0 = p; p += PF_TSLOT * PF_TS;
     sg1 = p; p += PF_TSLOT * PF_TS;
     rr = p; p += 4 * PF_TS;
@@ -289,8 +291,8 @@ struct TileIn {
 
 // Row pass of one evaluation (all waves): each wave leaves its beta-gradient
 // partials, segment sums and residual sums of squares in its LDS slots
-// (gb slot w & 1 — waves 2, 3 add onto waves 0, 1 after a barrier —, sg0/sg1
-// at segment + wave, rr[wave]); the segment slots were zeroed by the caller.
+// (gb[wave], sg0/sg1 at segment + wave, rr[wave]); the segment slots were
+// zeroed by the caller.
 template <int MODE, int KP>
 __device__ __forceinline__ void tile_rows(const FitKArgs &a, TileSmem<MODE, KP> &sm) {
   using Tr = TileTr<MODE, KP>;
@@ -322,8 +324,8 @@ __device__ __forceinline__ void tile_rows(const FitKArgs &a, TileSmem<MODE, KP> 
       const_cast<double *>(a.t), (short)0, Tp * 8, 0x00020000);
   const __amdgpu_buffer_rsrc_t rS = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<int32_t *>(a.seg), (short)0, Tp * 4, 0x00020000);
-  // y / cap rows of the slot's series (any series of the batch: 64-bit
-  // per-lane bases; an empty slot reads series 0 and masks it)
+  // y / cap rows of the slot's series (any series of the batch; an empty
+  // slot reads series 0 and masks it)
   const size_t srow = (size_t)(svalid ? s_g : 0) * Tp + 4 * rq;
   const pf_d2 *yb = reinterpret_cast<const pf_d2 *>(a.y_scaled + srow);
   const pf_d2 *cb = reinterpret_cast<const pf_d2 *>((LOGI ? a.cap_scaled : a.y_scaled) + srow);
@@ -383,14 +385,15 @@ __device__ __forceinline__ void tile_rows(const FitKArgs &a, TileSmem<MODE, KP> 
   int cur = -1;
   double *sl0 = sm.sg0 + wave * PF_TS + j, *sl1 = sm.sg1 + wave * PF_TS + j;  // slot s + wave
   // running sums of the current segment -> its slot (this wave is the only
-  // writer of slots s + wave: plain read-modify-write by lane rq = 0)
+  // writer of slots s + wave, so its LDS adds — no return value, no wait —
+  // apply in program order; lane rq = 0 adds)
   auto flush = [&]() {
     double b0 = a0 + shfl_xor_f64<16>(a0), b1 = a1 + shfl_xor_f64<16>(a1);
     b0 += shfl_xor_f64<32>(b0);
     b1 += shfl_xor_f64<32>(b1);
     if (rq == 0) {
-      sl0[cur * PF_TS] += b0;
-      sl1[cur * PF_TS] += b1;
+      atomicAdd(&sl0[cur * PF_TS], b0);
+      atomicAdd(&sl1[cur * PF_TS], b1);
     }
   };
   const int nch = (T + 15) >> 4;
@@ -474,28 +477,15 @@ __device__ __forceinline__ void tile_rows(const FitKArgs &a, TileSmem<MODE, KP> 
       a0 += (A0[0] + A0[1]) + (A0[2] + A0[3]);
       a1 += (A1[0] + A1[1]) + (A1[2] + A1[3]);
     } else {
-      // a chunk across segment boundaries (rare: one per changepoint at
-      // most): per segment, masked row sums reduced over rq, one writer
-      int s = s0;
-      while (true) {
-        double b0 = 0.0, b1 = 0.0;
-        bool more = false;
+      // a chunk across segment boundaries (at most one per changepoint):
+      // per-row adds into this wave's slots (a wave's LDS adds apply in
+      // instruction order, and the lanes of one add in lane order)
 #pragma unroll
-        for (int rg = 0; rg < 4; ++rg) {
-          const bool v = rbase + rg < T;
-          if (v && cu.sg[rg] == s) { b0 += A0[rg]; b1 += A1[rg]; }
-          more |= v && cu.sg[rg] > s;
+      for (int rg = 0; rg < 4; ++rg) {
+        if (rbase + rg < T) {
+          atomicAdd(&sl0[cu.sg[rg] * PF_TS], A0[rg]);
+          atomicAdd(&sl1[cu.sg[rg] * PF_TS], A1[rg]);
         }
-        b0 += shfl_xor_f64<16>(b0);
-        b1 += shfl_xor_f64<16>(b1);
-        b0 += shfl_xor_f64<32>(b0);
-        b1 += shfl_xor_f64<32>(b1);
-        if (rq == 0) {
-          sl0[s * PF_TS] += b0;
-          sl1[s * PF_TS] += b1;
-        }
-        if (__ballot(more) == 0ull) break;
-        ++s;
       }
     }
   };
@@ -516,30 +506,17 @@ __device__ __forceinline__ void tile_rows(const FitKArgs &a, TileSmem<MODE, KP> 
   rr += shfl_xor_f64<32>(rr);
   if (rq == 0) sm.rr[wave * PF_TS + j] = rr;
   // gradient tiles: C[row i = rq + 4 rg][series j] of tile ft is feature
-  // 2 i + ft (ft < 2) or 32 + i (ft = 2).  Waves 0, 1 store into slots 0, 1;
-  // after a barrier waves 2, 3 add theirs: a fixed summation order.
-  constexpr int SLOT = NSET * KP * PF_TS;
-  double *gsl = sm.gb + (wave & 1) * SLOT;
-  auto put = [&](bool add) {
+  // 2 i + ft (ft < 2) or 32 + i (ft = 2), stored into this wave's slot
+  double *gsl = sm.gb + wave * (NSET * KP * PF_TS);
 #pragma unroll
-    for (int ft = 0; ft < NFT; ++ft)
+  for (int ft = 0; ft < NFT; ++ft)
 #pragma unroll
-      for (int rg = 0; rg < 4; ++rg) {
-        const int i = rq + 4 * rg;
-        const int f = ft < 2 ? 2 * i + ft : 32 + i;
-        if constexpr (HM) {
-          double *d = gsl + f * PF_TS + j;
-          *d = add ? *d + gbm[ft][rg] : gbm[ft][rg];
-        }
-        if constexpr (HA) {
-          double *d = gsl + (NSET - 1) * KP * PF_TS + f * PF_TS + j;
-          *d = add ? *d + gba[ft][rg] : gba[ft][rg];
-        }
-      }
-  };
-  if (wave < 2) put(false);
-  __syncthreads();
-  if (wave >= 2) put(true);
+    for (int rg = 0; rg < 4; ++rg) {
+      const int i = rq + 4 * rg;
+      const int f = ft < 2 ? 2 * i + ft : 32 + i;
+      if constexpr (HM) gsl[f * PF_TS + j] = gbm[ft][rg];
+      if constexpr (HA) gsl[(NSET - 1) * KP * PF_TS + f * PF_TS + j] = gba[ft][rg];
+    }
 }
 
 // f and g of series j at xq (lane g: parameters g + 16 i -> gq), gpq =
@@ -632,7 +609,10 @@ __device__ __forceinline__ bool tile_assemble(const FitKArgs &a, TileSmem<MODE, 
     su0[2] = dpp_f64<PF_DPP_ROWBCAST(15)>(u0b);
     su1[2] = dpp_f64<PF_DPP_ROWBCAST(15)>(u1b);
   }
-  const double *gb0 = sm.gb, *gb1 = sm.gb + NSET * KP * PF_TS;
+  constexpr int GS = NSET * KP * PF_TS;
+  const double *gbw = sm.gb;
+  // beta-gradient slots of the four waves, added in wave order
+  auto gsum = [&](int off) { return (gbw[off] + gbw[GS + off]) + (gbw[2 * GS + off] + gbw[3 * GS + off]); };
   double fl = 0.0, gp = 0.0;
   bool bad = false;
 #pragma unroll
@@ -665,10 +645,8 @@ __device__ __forceinline__ bool tile_assemble(const FitKArgs &a, TileSmem<MODE, 
         const int f2 = p - 3 - S;
         const double sgm = sm.csg[f2];
         double gl = 0.0;
-        if constexpr (Tr::HM) gl += sm.csm[f2] * (gb0[f2 * PF_TS + j] + gb1[f2 * PF_TS + j]);
-        if constexpr (Tr::HA)
-          gl += sm.csa[f2] * (gb0[(NSET - 1) * KP * PF_TS + f2 * PF_TS + j] +
-                              gb1[(NSET - 1) * KP * PF_TS + f2 * PF_TS + j]);
+        if constexpr (Tr::HM) gl += sm.csm[f2] * gsum(f2 * PF_TS + j);
+        if constexpr (Tr::HA) gl += sm.csa[f2] * gsum((NSET - 1) * KP * PF_TS + f2 * PF_TS + j);
         gv = -inv * gl + xv / (sgm * sgm);
         ft = xv * xv / (2.0 * sgm * sgm);
       }
@@ -986,7 +964,7 @@ __device__ __forceinline__ bool tile_load_series(const FitKArgs &a, TileSmem<MOD
 // Pass-0 semantics of fit_body (theta in: init; out: the L-BFGS endpoint,
 // f, f_stan, status, n_iter, n_eval); warm = the iteration cap is the
 // warm-up cap (MAXIT -> WARMUP).
-// Per evaluation: row pass (all waves; one internal barrier) | barrier |
+// Per evaluation: row pass (all waves) | barrier |
 // assemble (16 lanes per series) | barrier | zero segment slots + L-BFGS
 // step (+ outputs and refill) + publish | barrier.
 template <int MODE, int KP>

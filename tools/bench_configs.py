@@ -29,7 +29,18 @@ def main():
     ap.add_argument("--method", default=None, help="interval method (default per config)")
     ap.add_argument("--tile-min", type=int, default=None,
                     help="pf_fit_opts.tile_min_series (default: the engine's, 2048; -1 disables K3T)")
+    ap.add_argument("--tail", default=None,
+                    help="write the series that end without PF_ST_MAP (status, evaluations, f, "
+                         "the engine's Stan-phase f, inputs; at most 64) to this .npz for "
+                         "tools/tail_oracle.py")
+    ap.add_argument("--e-sample", type=int, default=2048,
+                    help="series of the Stan-faithful (stan_map) run that estimates the "
+                         "algorithmic evaluation count E (0: skip)")
+    ap.add_argument("--lib", default=None, help="load this engine library instead (A/B runs)")
     args = ap.parse_args()
+    if args.lib:
+        from distributed_forecasting_amd import _lib
+        _lib.load(os.path.abspath(args.lib))
     import torch
     import distributed_forecasting_amd as dfa
     from distributed_forecasting_amd import batch as B, holidays as H, synthetic
@@ -106,20 +117,80 @@ def main():
     stats = []
     for k in range(len(chunks)):
         fit, out = run(k)
-        stats.append((fit.n_eval, fit.status))   # reduced after the timed region
+        stats.append((fit.n_eval, fit.status, fit.f, fit.f_stan))   # reduced after the timed region
         print(f"chunk {k + 1}/{len(chunks)}", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    stats = [(ne.double().mean().item(), (st == 70).double().mean().item()) for ne, st in stats]
     kern = {}
     for name, ms, _ in eng.ctx.read_timings():
         kern[name] = kern.get(name, 0.0) + ms
     eng.ctx.set_timing(False)
+    n_eval_all = torch.cat([s_[0] for s_ in stats]).double()
+    status_all = torch.cat([s_[1] for s_ in stats])
+    evals_performed = float(n_eval_all.sum().item())
+    tail = {"n_uncertified": int((status_all != 70).sum().item()),
+            "status_counts": {int(v): int(c) for v, c in zip(*np.unique(status_all.cpu().numpy(),
+                                                                         return_counts=True))}}
+    if args.tail and tail["n_uncertified"]:
+        f_all = torch.cat([s_[2] for s_ in stats]).cpu().numpy()
+        fs_all = torch.cat([s_[3] for s_ in stats]).cpu().numpy()
+        st_np = status_all.cpu().numpy()
+        bad = np.flatnonzero(st_np != 70)[:64]
+        ys, cs = [], []
+        gen = {}
+        for i in bad:
+            k = next(kk for kk, (a, b) in enumerate(chunks) if a <= i < b)
+            if args.config == 5:
+                if k not in gen:       # each chunk's generator run once
+                    gen = {k: synthetic.saturating_matrix(chunks[k][1] - chunks[k][0], ds,
+                                                          seed=20261015 + 4 + k)}
+                    print(f"tail: regenerated chunk {k + 1}", file=sys.stderr, flush=True)
+                Yk, ck = gen[k]
+                ys.append(Yk[i - chunks[k][0]].copy())
+                cs.append(ck[i - chunks[k][0]].copy())
+            else:
+                ys.append(Y[i])
+        np.savez_compressed(args.tail, index=bad, status=st_np[bad], n_eval=n_eval_all.cpu().numpy()[bad],
+                            f=f_all[bad], f_stan_engine=fs_all[bad], y=np.stack(ys), ds=ds,
+                            cap=np.stack(cs) if cs else np.zeros(0), config=args.config)
+        tail["dump"] = args.tail
+    # SURVEY §8d algorithmic work: E (the Stan-faithful evaluation count per
+    # series) x 4T(F + 2C) per evaluation.  E is estimated from the engine's
+    # Stan-faithful run (fit_mode stan_map's first pass: Stan's termination
+    # rules, the oracle's control flow) on a sample; frac_performed uses the
+    # evaluations the engine actually ran.
+    fit_k = "k_fit_tile" if "k_fit_tile" in kern else ("k_fit_polish" if "k_fit_polish" in kern else "k_fit")
+    flop_eval = 4.0 * T * (grid.K + 2 * grid.S)
+    roof = None
+    if args.e_sample > 0:
+        m = min(args.e_sample, chunks[0][1] - chunks[0][0])
+        Ys = Yd[0][:m].clone()
+        cs_ = capd[0][:m].clone() if capd is not None else None
+        print(f"E sample: {m} series, Stan-faithful run", file=sys.stderr, flush=True)
+        fs = eng.fit(grid, Ys, cap=cs_, polish=False)
+        E_mean = float(fs.n_eval.double().mean().item())
+        fit_s = kern.get(fit_k, float("nan")) / 1e3
+        alg = E_mean * n * flop_eval
+        perf = evals_performed * flop_eval
+        roof = {"kernel": fit_k, "kernel_s_total": fit_s, "flop_per_eval": flop_eval,
+                "E_stan_faithful_mean": E_mean, "E_sample": m,
+                "evals_performed_mean": evals_performed / n,
+                "achieved_tflops": alg / fit_s / 1e12, "peak_tflops": 78.6,
+                "frac": alg / fit_s / 1e12 / 78.6,
+                "achieved_performed_tflops": perf / fit_s / 1e12,
+                "frac_performed": perf / fit_s / 1e12 / 78.6,
+                "note": ("frac: SURVEY §8d algorithmic FLOPs (E = Stan-faithful evaluations per series, "
+                         "estimated on a sample) over the fit kernel's time; it exceeds frac_performed "
+                         "when the engine runs fewer evaluations than Stan (warm-up hand-off to the "
+                         "polish) — a frac above 1 is credit for skipped evaluations, not hardware "
+                         "rate; frac_performed is the rate on the evaluations actually run")}
+    stats = [(ne.double().mean().item(), (st == 70).double().mean().item()) for ne, st, _, _ in stats]
     res = {"metric": "series fit+forecast/sec", "config_index": args.config, "value": n / el,
            "unit": "series/s", "n_gpus": 1, "seconds": el, "workload": work, "chunk": chunk,
            "kernels_ms_total": kern, "tile_min_series": args.tile_min,
            "n_eval_mean": float(np.mean([s[0] for s in stats])),
            "map_certified": float(np.mean([s[1] for s in stats])),
+           "roofline": roof, "uncertified": tail,
            "data": "synthetic (SURVEY.md §8d generators)"}
     print(json.dumps(res))
 

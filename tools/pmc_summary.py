@@ -30,12 +30,13 @@ def main(src, tag):
     os.makedirs(prof, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
                 os.path.join(prof, f"{tag}_kernel_stats.csv"))
+    keep_fit = len(sys.argv) < 4 or sys.argv[3] != "--no-fit-traffic"
     out = defaultdict(dict)
     with open(os.path.join(src, "trace", "run_kernel_stats.csv")) as f:
         for row in csv.DictReader(f):
             out[row["Name"]]["avg_ns"] = float(row["AverageNs"])
             out[row["Name"]]["calls"] = int(row["Calls"])
-    for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_mfma"):
+    for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_mfma", "pmc_lds"):
         p = os.path.join(src, sub, "run_counter_collection.csv")
         if not os.path.exists(p):
             continue
@@ -58,12 +59,14 @@ def main(src, tag):
         if "SQ_INSTS_VALU_MFMA_MOPS_F64" in d:
             # one MOP = 512 FLOP (gfx9 MFMA MOPS unit); 16x16x4 f64 = 2048 FLOP = 4 MOPS
             d["mfma_f64_flops_per_launch"] = 512.0 * d["SQ_INSTS_VALU_MFMA_MOPS_F64"]
+        if d.get("SQ_ACTIVE_INST_LDS", 0) > 0 and "SQ_LDS_BANK_CONFLICT" in d:
+            d["lds_bank_conflict_per_active_lds"] = d["SQ_LDS_BANK_CONFLICT"] / d["SQ_ACTIVE_INST_LDS"]
         if "SQ_VALU_MFMA_BUSY_CYCLES" in d and d.get("SQ_BUSY_CU_CYCLES", 0) > 0:
             d["mfma_busy_per_cu_busy"] = d["SQ_VALU_MFMA_BUSY_CYCLES"] / d["SQ_BUSY_CU_CYCLES"]
     with open(os.path.join(prof, f"{tag}_pmc.json"), "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
     kf = "k_fit_polish" if "k_fit_polish" in out else "k_fit"
-    if kf in out and "hbm_bytes_per_launch" in out[kf]:
+    if keep_fit and kf in out and "hbm_bytes_per_launch" in out[kf]:
         with open(os.path.join(prof, "pmc_k_fit.json"), "w") as f:
             json.dump({"tag": tag, "kernel": kf,
                        "hbm_bytes_per_launch": out[kf]["hbm_bytes_per_launch"],
@@ -71,7 +74,7 @@ def main(src, tag):
                        "WRITE_SIZE_KiB": out[kf]["WRITE_SIZE"],
                        "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE half-count)"},
                       f, indent=1)
-    for k in ("k_fit", "k_fit_polish", "k_polish", "k_predict_det", "k_predict_mc"):
+    for k in ("k_fit", "k_fit_polish", "k_fit_tile", "k_polish", "k_predict_det", "k_predict_mc"):
         if k in out:
             print(k, {a: (round(b, 4) if isinstance(b, float) else b) for a, b in out[k].items()})
 

@@ -13,17 +13,32 @@ _lib.load(os.path.abspath(out))
 import distributed_forecasting_amd as dfa
 from distributed_forecasting_amd import synthetic
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
-ds = synthetic.daily_dates(); Y = synthetic.sales_matrix(n, ds, config_index=2)
-eng = dfa.Engine(0)
-seasons = eng.config.seasons(int(ds[0]), int(ds[-1]), int(ds[1] - ds[0]))
-grid = dfa.build_grid(ds, seasons, start_ns=int(ds[0]), t_scale_ns=int(ds[-1] - ds[0]))
+c4 = len(sys.argv) > 2 and sys.argv[2] == "c4"     # configs[4]: hourly logistic, P = 72
+cap = None
+if c4:
+    from distributed_forecasting_amd import holidays as H
+    from distributed_forecasting_amd.engine import ProphetConfig
+    cfg = ProphetConfig.reference()
+    cfg.growth = "logistic"
+    ds = synthetic.hourly_dates(n_hours=8760)
+    Y, cp = synthetic.saturating_matrix(n, ds)
+    eng = dfa.Engine(0, cfg)
+    seasons = [("yearly", 365.25, 10), ("weekly", 7.0, 3), ("daily", 1.0, 4)]
+    hol = H.holiday_spec(H.synthetic_holidays([2017, 2018]), 10.0)
+    grid = dfa.build_grid(ds, seasons, start_ns=int(ds[0]), t_scale_ns=int(ds[-1] - ds[0]), holidays=hol)
+    cap = torch.zeros((n, grid.T_pad), dtype=torch.float64, device="cuda"); cap[:, :grid.T] = torch.from_numpy(cp).cuda()
+else:
+    ds = synthetic.daily_dates(); Y = synthetic.sales_matrix(n, ds, config_index=2)
+    eng = dfa.Engine(0)
+    seasons = eng.config.seasons(int(ds[0]), int(ds[-1]), int(ds[1] - ds[0]))
+    grid = dfa.build_grid(ds, seasons, start_ns=int(ds[0]), t_scale_ns=int(ds[-1] - ds[0]))
 Yd = torch.zeros((n, grid.T_pad), dtype=torch.float64, device="cuda"); Yd[:, :grid.T] = torch.from_numpy(Y).cuda()
 lib = _lib._lib
 buf = (ctypes.c_ulonglong * 32)()
-eng.fit(grid, Yd, polish=False, tile_min_series=1); torch.cuda.synchronize()
+eng.fit(grid, Yd, cap=cap, polish=False, tile_min_series=1); torch.cuda.synchronize()
 lib.pf_debug_stamps(buf, 1)
 t0 = time.time()
-fit = eng.fit(grid, Yd, polish=False, tile_min_series=1, lbfgs_warmup=0); torch.cuda.synchronize()
+fit = eng.fit(grid, Yd, cap=cap, polish=False, tile_min_series=1, lbfgs_warmup=0); torch.cuda.synchronize()
 dt = time.time() - t0
 lib.pf_debug_stamps(buf, 1)
 v = np.array(list(buf), dtype=np.float64)
