@@ -203,8 +203,27 @@ def _stan_evals(args):
     return ne, f, status
 
 
+def c4_uncertified_fixture(tail_npz, n=2):
+    """Series of configs[4] that ended without PF_ST_MAP in a full-scale run
+    (tools/bench_configs.py 5 --tail; synthetic.saturating_matrix rows), with
+    the oracle's Stan endpoint objective (tools/tail_oracle.py's check):
+    golden_c4_uncertified.npz."""
+    import sys as _sys
+    _sys.path.insert(0, os.path.join(os.path.dirname(OUT), "..", "tools"))
+    from tail_oracle import _one
+    z = np.load(tail_npz, allow_pickle=False)
+    res = [_one((5, z["ds"], z["y"][i], z["cap"][i])) for i in range(n)]
+    np.savez_compressed(os.path.join(OUT, "golden_c4_uncertified.npz"), ds=z["ds"], y=z["y"][:n],
+                        cap=z["cap"][:n], index=z["index"][:n], status_full_run=z["status"][:n],
+                        f_oracle_stan=np.array([r[0] for r in res]),
+                        f_oracle_polished=np.array([r[3] for r in res]))
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["reference", "edge", "bench", "configs4", "stan64"]
+    if which[0] == "c4tail":            # c4tail <tools/bench_configs.py --tail npz>
+        c4_uncertified_fixture(which[1])
+        sys.exit(0)
     if "reference" in which:
         reference_fixture()
     if "edge" in which:
@@ -215,3 +234,4 @@ if __name__ == "__main__":
         configs4_fixture()
     if "stan64" in which:
         stan64_fixture()
+
