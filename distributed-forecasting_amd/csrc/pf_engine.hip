@@ -2768,9 +2768,25 @@ int pf_predict(pf_ctx *ctx, const pf_predict_args *p, void *stream) {
       if (gx < 1) gx = 1;
     }
     const dim3 gmc(gx, a.n_series);
-    PF_TIMED_LAUNCH(ctx, "k_predict_mc", gmc.x * gmc.y, (hipStream_t)stream,
-                    (k_predict_mc<64>), gmc, dim3(PF_MC_WAVES * 64), 0, (hipStream_t)stream, a);
+    if (a.tr)
+      PF_TIMED_LAUNCH(ctx, "k_predict_mc", gmc.x * gmc.y, (hipStream_t)stream,
+                      (k_predict_mc<64, true>), gmc, dim3(PF_MC_WAVES * 64), 0, (hipStream_t)stream, a);
+    else
+      PF_TIMED_LAUNCH(ctx, "k_predict_mc", gmc.x * gmc.y, (hipStream_t)stream,
+                      (k_predict_mc<64, false>), gmc, dim3(PF_MC_WAVES * 64), 0, (hipStream_t)stream, a);
     PF_HIP(ctx, hipGetLastError());
+    if (a.method == PF_INTERVAL_SAMPLE) {
+      // the deterministic-trend rows' samples (k_predict_mc walks the random rows)
+      // a block per series (its setup once) when the series alone fill the
+      // GPU, more blocks (each wave a strided set of 64-row chunks) otherwise
+      int hx = (a.Tf + 64 * PF_MC_WAVES - 1) / (64 * PF_MC_WAVES);
+      const int hwant = (16384 + a.n_series - 1) / a.n_series;
+      if (hx > hwant) hx = hwant;
+      const dim3 gh(hx, a.n_series);
+      PF_TIMED_LAUNCH(ctx, "k_predict_mc_hist", gh.x * gh.y, (hipStream_t)stream,
+                      (k_predict_mc_hist<64>), gh, dim3(PF_MC_WAVES * 64), 0, (hipStream_t)stream, a);
+      PF_HIP(ctx, hipGetLastError());
+    }
   }
   return 0;
 }

@@ -162,6 +162,7 @@ __device__ __forceinline__ int wave_prefix_i32(int v) {
 // general wave_tail_select).  Absent samples are NaN (never beyond).
 __device__ __forceinline__ bool wave_tail_select_z(const float (&z)[PF_NQ], const int (&kk)[2], float zthr,
                                                    float *buf, float (&o0)[2], float (&o1)[2]) {
+  // buf: 2 * 64 floats of wave-private LDS
   const int lane = pf_lane();
   int c0 = 0, c1 = 0;
 #pragma unroll
@@ -259,10 +260,42 @@ __device__ __forceinline__ float mc_trend_direct(uint32_t seed0, uint32_t seed1,
   return (float)(capy / (1.0 + exp(-(kc * (1.0 + tau - mc)))));
 }
 
-// The wave's rows [row_b, row_e).  DIRECT: every trend sample re-derived from
-// the stream (s_meta = count); otherwise the per-sample running state over
-// the packed changepoints.
-template <bool DIRECT>
+// The lane's PF_NQ standard-normal noise draws of one row (sample lane + 64 q;
+// absent samples, lane + 64 q >= N, are NaN): 16 uniforms of 24 bits from 12
+// Philox words (three calls keyed (call, lane, row, series); each word's top
+// 24 bits, the fourth uniform of a group of three words from their low
+// bytes), Box-Muller pairs.
+__device__ __forceinline__ void mc_row_normals(const PredKArgs &a, uint32_t sid, int row, float (&z)[PF_NQ]) {
+  const int lane = pf_lane();
+  uint32_t uw[PF_NQ];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const pf_u4 rr = philox4x32_10(pf_u4{(uint32_t)c, (uint32_t)lane, (uint32_t)row, sid}, a.seed0, a.seed1);
+    const uint32_t w[4] = {rr.x, rr.y, rr.z, rr.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      // words 4c + j: groups g = (4c + j) / 3 of three words
+      const int wi = 4 * c + j, g = wi / 3, m = wi % 3;
+      uw[4 * g + m] = w[j];
+      if (m == 0) uw[4 * g + 3] = (w[j] & 0xFFu) << 8;
+      else uw[4 * g + 3] |= (w[j] & 0xFFu) << (8 + 8 * m);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < PF_NQ / 4; ++c) {
+    pf_box_muller(pf_u01f(uw[4 * c]), pf_u01f(uw[4 * c + 1]), z[4 * c], z[4 * c + 1]);
+    pf_box_muller(pf_u01f(uw[4 * c + 2]), pf_u01f(uw[4 * c + 3]), z[4 * c + 2], z[4 * c + 3]);
+  }
+#pragma unroll
+  for (int q = 0; q < PF_NQ; ++q)
+    if (lane + 64 * q >= a.N) z[q] = __builtin_nanf("");
+}
+
+// The wave's rows [row_b, row_e), every one a random-trend row (t > 1; the
+// deterministic-trend rows are k_predict_det's (exact) or k_predict_mc_hist's
+// (sample)).  DIRECT: every trend sample re-derived from the stream (s_meta =
+// count); otherwise the per-sample running state over the packed changepoints.
+template <bool DIRECT, bool TR>
 __device__ __forceinline__ void mc_rows(const PredKArgs &a, const PredSeries &ps, const float2 *s_cp,
                                         const uint32_t *s_meta, float *buf, int series, uint32_t sid,
                                         double t_max, int row_b, int row_e) {
@@ -307,9 +340,8 @@ __device__ __forceinline__ void mc_rows(const PredKArgs &a, const PredSeries &ps
     }
     const double l_trend = trs * ysc, l_add = xba * ysc;
     const float lf_tau = (float)(ti - 1.0), lf_trend = (float)l_trend, lf_u1 = (float)(1.0 + xbm);
-    const float lf_add = (float)l_add, lf_yhat = (float)(l_trend * (1.0 + xbm) + l_add);
+    const float lf_add = (float)l_add;
     const float lf_capy = (float)(ysc * capr);
-    const int l_rand = (rv && pred_row_random(a, ti, t_max)) ? 1 : 0;
     float o_ylo = 0.f, o_yhi = 0.f, o_tlo = 0.f, o_thi = 0.f;
     PF_STAMP1(2);
     for (int r = 0; r < nr; ++r) {
@@ -319,19 +351,22 @@ __device__ __forceinline__ void mc_rows(const PredKArgs &a, const PredSeries &ps
       const float tau = readlane_f32(lf_tau, r);
       const float trendf = readlane_f32(lf_trend, r);
       const float u1 = readlane_f32(lf_u1, r), addf = readlane_f32(lf_add, r);
-      const bool random = __builtin_amdgcn_readlane(l_rand, r) != 0;
-      const float yh = readlane_f32(lf_yhat, r);
-      float v[PF_NQ], tv[PF_NQ];
+      // v: the yhat samples; tv: the trend samples (kept only for trend bands)
+      float v[PF_NQ], tv[TR ? PF_NQ : 1];
       float ylo, yhi, tlo = trendf, thi = trendf;
-      if (random) {
+      float z[PF_NQ];
+      {
         const float capy = readlane_f32(lf_capy, r);
         if constexpr (DIRECT) {
+          mc_row_normals(a, sid, row, z);
 #pragma unroll
           for (int q = 0; q < PF_NQ; ++q) {
             const int smp = lane + 64 * q;
-            tv[q] = (smp < N) ? mc_trend_direct(a.seed0, a.seed1, sid, smp, (int)s_meta[smp], t_max, lam,
-                                                (double)tau, logi, (double)trendf, ysc, (double)capy, k0, m0)
-                              : __builtin_nanf("");
+            const float ts = (smp < N) ? mc_trend_direct(a.seed0, a.seed1, sid, smp, (int)s_meta[smp], t_max, lam,
+                                                         (double)tau, logi, (double)trendf, ysc, (double)capy, k0, m0)
+                                       : __builtin_nanf("");
+            if constexpr (TR) tv[q] = ts;
+            v[q] = (smp < N) ? fmaf(sd, z[q], fmaf(ts, u1, addf)) : __builtin_nanf("");
           }
         } else {
           // absorb the changepoints passed since the previous row: one pass
@@ -366,61 +401,22 @@ __device__ __forceinline__ void mc_rows(const PredKArgs &a, const PredSeries &ps
             if (more == 0ull) break;
           }
           PF_STAMP1(4);
+          mc_row_normals(a, sid, row, z);
+          PF_STAMP1(5);
           const float ysf = (float)ysc;
 #pragma unroll
           for (int q = 0; q < PF_NQ; ++q) {
             float trs_s;
             if (!logi) trs_s = fmaf(ysf, fmaf(s1[q], tau, -s2[q]), trendf);
             else trs_s = (st[q] & PF_MC_ABS) ? capy / (1.0f + __expf(-(s1[q] * (1.0f + tau - s2[q])))) : trendf;
-            tv[q] = (lane + 64 * q < N) ? trs_s : __builtin_nanf("");
-          }
-        }
-      }
-      PF_STAMP1(5);
-      float zs[PF_NQ];
-      // the lane's 16 noise draws: 16 uniforms of 24 bits from 12 Philox
-      // words (three calls; each word's top 24 bits, the fourth uniform of a
-      // group from the three low bytes), Box-Muller pairs
-      uint32_t uw[PF_NQ];
-#pragma unroll
-      for (int c = 0; c < PF_NQ / 4; c += 1) {
-        if (c < 3) {
-          const pf_u4 rr = philox4x32_10(pf_u4{(uint32_t)c, (uint32_t)lane, (uint32_t)row, sid},
-                                         a.seed0, a.seed1);
-          const uint32_t w[4] = {rr.x, rr.y, rr.z, rr.w};
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            // words 4c + j, c < 3: groups g = (4c + j) / 3 of three words
-            const int wi = 4 * c + j, g = wi / 3, m = wi % 3;
-            uw[4 * g + m] = w[j];
-            if (m == 0) uw[4 * g + 3] = (w[j] & 0xFFu) << 8;
-            else uw[4 * g + 3] |= (w[j] & 0xFFu) << (8 + 8 * m);
-          }
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < PF_NQ / 4; ++c) {
-        float z[4];
-        pf_box_muller(pf_u01f(uw[4 * c]), pf_u01f(uw[4 * c + 1]), z[0], z[1]);
-        pf_box_muller(pf_u01f(uw[4 * c + 2]), pf_u01f(uw[4 * c + 3]), z[2], z[3]);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int q = 4 * c + j;
-          v[q] = random ? fmaf(sd, z[j], fmaf(tv[q], u1, addf)) : fmaf(sd, z[j], yh);
-          zs[q] = z[j];
-          if (lane + 64 * q >= N) {
-            v[q] = __builtin_nanf("");
-            zs[q] = __builtin_nanf("");
+            const bool on = lane + 64 * q < N;
+            if constexpr (TR) tv[q] = on ? trs_s : __builtin_nanf("");
+            v[q] = on ? fmaf(sd, z[q], fmaf(trs_s, u1, addf)) : __builtin_nanf("");
           }
         }
       }
       PF_STAMP1(6);
-      float zo0[2], zo1[2];
-      if (!random && a.zthr > 0.0f && wave_tail_select_z(zs, kk2, a.zthr, buf, zo0, zo1)) {
-        // order statistics of yhat + sd z: the same monotone map of z's
-        ylo = np_lerp(fmaf(sd, zo0[0], yh), fmaf(sd, zo1[0], yh), a.fr_lo);
-        yhi = np_lerp(fmaf(sd, -zo1[1], yh), fmaf(sd, -zo0[1], yh), a.fr_hi);
-      } else if (random && a.tr) {
+      if constexpr (TR) {
         float o0[4], o1[4];
         wave_tail_select<4>(v, tv, kk4, buf, o0, o1);
         if (N == 1) { for (int s = 0; s < 4; ++s) o1[s] = o0[s]; }
@@ -429,7 +425,7 @@ __device__ __forceinline__ void mc_rows(const PredKArgs &a, const PredSeries &ps
         tlo = np_lerp(o0[2], o1[2], a.fr_lo);
         thi = np_lerp(-o1[3], -o0[3], a.fr_hi);
       } else {
-        // yhat tails only (deterministic rows, or no trend bands requested)
+        // yhat tails only (no trend bands requested)
         float o0[2], o1[2];
         wave_tail_select<2>(v, v, kk2, buf, o0, o1);
         if (N == 1) { o1[0] = o0[0]; o1[1] = o0[1]; }
@@ -448,7 +444,7 @@ __device__ __forceinline__ void mc_rows(const PredKArgs &a, const PredSeries &ps
   }
 }
 
-template <int KMAX>
+template <int KMAX, bool TR>
 __global__ __launch_bounds__(PF_MC_WAVES * 64) void k_predict_mc(PredKArgs a0) {
   PredKArgs a = a0;
   if (a0.grid_of) bind_pred_grid(a, blockIdx.y);
@@ -464,11 +460,11 @@ __global__ __launch_bounds__(PF_MC_WAVES * 64) void k_predict_mc(PredKArgs a0) {
   const uint32_t sid = a.series_id ? a.series_id[series] : (uint32_t)series;
   const int N = a.N;
   PF_STAMP1(0);
-  if (tid == 0) s_r0 = (a.method == PF_INTERVAL_SAMPLE) ? 0 : a.Tf;
+  if (tid == 0) s_r0 = a.Tf;
   pred_setup(a, series, ps);
   const double t_max = a.t[a.Tf - 1];
   __syncthreads();
-  if (a.method != PF_INTERVAL_SAMPLE) {
+  {
     // first random-trend row (rows sorted by t): independent loads, min
     int loc = a.Tf;
     for (int b0 = 0; b0 < a.Tf; b0 += 8 * NT) {
@@ -534,6 +530,88 @@ __global__ __launch_bounds__(PF_MC_WAVES * 64) void k_predict_mc(PredKArgs a0) {
   const int row_b = r0 + (blockIdx.x * PF_MC_WAVES + wave) * rpw;
   const int row_e = min(row_b + rpw, a.Tf);
   if (row_b >= row_e) return;  // no block-level sync below
-  if (ovf) mc_rows<true>(a, ps, s_cp, s_meta, s_buf[wave], series, sid, t_max, row_b, row_e);
-  else mc_rows<false>(a, ps, s_cp, s_meta, s_buf[wave], series, sid, t_max, row_b, row_e);
+  if (ovf) mc_rows<true, TR>(a, ps, s_cp, s_meta, s_buf[wave], series, sid, t_max, row_b, row_e);
+  else mc_rows<false, TR>(a, ps, s_cp, s_meta, s_buf[wave], series, sid, t_max, row_b, row_e);
+}
+
+// ---- sample mode, deterministic-trend rows (the history: t <= 1, or every
+// row under flat growth).  UPSTREAM's samples of such a row are yhat + sd z_i
+// (no new changepoints), so nothing carries from row to row: a wave walks
+// 64-row chunks (chunk = wave index + k x the grid's waves) with no
+// per-sample changepoint state, setup or block-level sync in the row loop,
+// which keeps the kernel far below k_predict_mc's registers (more waves per
+// SIMD to hide the Philox / Box-Muller / selection latency chains).  The
+// draws and the selection are k_predict_mc's row arithmetic (mc_row_normals,
+// the threshold selection on z, the general wave_tail_select otherwise):
+// the intervals are bitwise those of one kernel walking every row.  Rows are
+// sorted by t, so the deterministic rows are a prefix: a wave stops at its
+// first chunk without one (k_predict_mc writes the random rows).
+// Grid (<= ceil(Tf / (64 PF_MC_WAVES)), n_series).
+template <int KMAX>
+__global__ __launch_bounds__(PF_MC_WAVES * 64) void k_predict_mc_hist(PredKArgs a0) {
+  PredKArgs a = a0;
+  if (a0.grid_of) bind_pred_grid(a, blockIdx.y);
+  __shared__ PredSeries ps;
+  __shared__ float s_buf[PF_MC_WAVES][2 * 64];
+  const int series = blockIdx.y, lane = pf_lane(), wave = pf_wave();
+  const int nchunk = (a.Tf + 63) / 64;
+  if ((int)blockIdx.x * PF_MC_WAVES >= nchunk) return;  // uniform per block (ragged grids)
+  const uint32_t sid = a.series_id ? a.series_id[series] : (uint32_t)series;
+  const int N = a.N;
+  pred_setup(a, series, ps);
+  __syncthreads();
+  const double t_max = a.t[a.Tf - 1];
+  const double ysc = ps.ysc;
+  const float sd = (float)(ps.sigma * ysc);
+  const int kk2[2] = {a.k_lo, a.k_hi_neg};
+  float *buf = s_buf[wave];
+  for (int ch = blockIdx.x * PF_MC_WAVES + wave; ch < nchunk; ch += gridDim.x * PF_MC_WAVES) {
+    const int c0 = ch * 64;
+    const int nr = min(64, a.Tf - c0);
+    const int myrow = c0 + lane;
+    const bool rv = lane < nr;
+    // lane-per-row deterministic part (k_predict_mc's arithmetic)
+    double ti = 0.0, xbm = 0.0, xba = 0.0, trs = 0.0;
+    if (rv) {
+      ti = a.t[myrow];
+      pred_row_dot(a, ps, myrow, xbm, xba);
+      trs = pred_trend(a, ps, series, myrow, ti, a.seg[myrow]);
+    }
+    const double l_trend = trs * ysc, l_add = xba * ysc;
+    const float lf_trend = (float)l_trend, lf_yhat = (float)(l_trend * (1.0 + xbm) + l_add);
+    const bool mine = rv && !pred_row_random(a, ti, t_max);
+    unsigned long long todo = __ballot(mine);
+    if (todo == 0ull) break;
+    float o_ylo = 0.f, o_yhi = 0.f;
+    while (todo) {
+      const int r = __builtin_ctzll(todo);
+      todo &= todo - 1ull;
+      const int row = c0 + r;
+      const float yh = readlane_f32(lf_yhat, r);
+      float z[PF_NQ];
+      mc_row_normals(a, sid, row, z);
+      float ylo, yhi;
+      float zo0[2], zo1[2];
+      if (a.zthr > 0.0f && wave_tail_select_z(z, kk2, a.zthr, buf, zo0, zo1)) {
+        // order statistics of yhat + sd z: the same monotone map of z's
+        ylo = np_lerp(fmaf(sd, zo0[0], yh), fmaf(sd, zo1[0], yh), a.fr_lo);
+        yhi = np_lerp(fmaf(sd, -zo1[1], yh), fmaf(sd, -zo0[1], yh), a.fr_hi);
+      } else {
+        float v[PF_NQ], o0[2], o1[2];
+#pragma unroll
+        for (int q = 0; q < PF_NQ; ++q) v[q] = (lane + 64 * q < N) ? fmaf(sd, z[q], yh) : __builtin_nanf("");
+        wave_tail_select<2>(v, v, kk2, buf, o0, o1);
+        if (N == 1) { o1[0] = o0[0]; o1[1] = o0[1]; }
+        ylo = np_lerp(o0[0], o1[0], a.fr_lo);
+        yhi = np_lerp(-o1[1], -o0[1], a.fr_hi);
+      }
+      if (lane == r) { o_ylo = ylo; o_yhi = yhi; }
+    }
+    if (mine) {
+      const size_t o = (size_t)series * a.Tp + myrow;
+      a.ylo[o] = o_ylo;
+      a.yhi[o] = o_yhi;
+      if (a.tr) { a.trlo[o] = lf_trend; a.trhi[o] = lf_trend; }
+    }
+  }
 }

@@ -36,7 +36,7 @@ def main(src, tag):
         for row in csv.DictReader(f):
             out[row["Name"]]["avg_ns"] = float(row["AverageNs"])
             out[row["Name"]]["calls"] = int(row["Calls"])
-    for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_mfma", "pmc_lds"):
+    for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_mfma", "pmc_lds", "pmc_valu"):
         p = os.path.join(src, sub, "run_counter_collection.csv")
         if not os.path.exists(p):
             continue
