@@ -57,6 +57,7 @@ N_SAMPLES = 1000
 SERIES_PER_GPU = 500
 C2_SERIES = 50_000
 FLOPS_PER_EVAL = 4 * T_DAYS * (26 + 2 * 25)      # 555,104
+PEAK_VALU_GINSTS = 1024 * 2.4 / 2    # wave64 VALU instructions per ns, whole GPU
 PEAK_FP64_TFLOPS = 78.6                            # MI355X FP64 (vector = matrix), SURVEY.md §8d
 PEAK_HBM_GBS = 8000.0
 
@@ -359,13 +360,31 @@ def main():
                 "time; frac_performed = the kernel-efficiency figure on the L-BFGS evaluations "
                 "the engine performed; traffic = HBM bytes per launch from rocprofv3 PMC "
                 "(profiles/pmc_k_fit.json)"}
-    pred_bytes = 16.0 * len(fut) * n                # yhat, lo, hi, trend fp32 per row
-    pred_s = (kern_avg.get("k_predict_det", float("nan")) + kern_avg.get("k_predict_mc", 0.0)) / 1e3
-    res["forecast_roofline"] = {"bound": "hbm", "kernel": "k_predict_det + k_predict_mc",
-                                "achieved": pred_bytes / pred_s / 1e9, "peak": PEAK_HBM_GBS,
-                                "unit": "GB/s", "frac": pred_bytes / pred_s / 1e9 / PEAK_HBM_GBS,
-                                "note": "algorithmic output bytes only; the kernels are "
-                                        "VALU-bound (RNG + order statistics)"}
+    # K5 (the Monte-Carlo future rows, the longest forecast kernel) is
+    # VALU-issue-bound work (Philox, Box-Muller, wave sorts): its roofline is
+    # the vector-instruction issue rate, one wave64 VALU instruction per 2
+    # cycles per SIMD (1024 SIMDs at 2.4 GHz), with the instruction count per
+    # launch from rocprofv3 PMC (SQ_INSTS_VALU, profiles/pmc_k_predict_mc.json,
+    # same launch shape) over the live kernel time
+    mc_ms = kern_avg.get("k_predict_mc")
+    mc_pmc = None
+    mc_path = os.path.join(ROOT, "profiles", "pmc_k_predict_mc.json")
+    if os.path.exists(mc_path):
+        with open(mc_path) as f:
+            mc_pmc = json.load(f)
+    if mc_ms and mc_pmc and mc_pmc.get("n_series") == n and mc_pmc.get("horizon") == HORIZON:
+        insts = float(mc_pmc["SQ_INSTS_VALU"])
+        ach = insts / (mc_ms / 1e3)
+        res["forecast_roofline"] = {
+            "bound": "valu-issue", "kernel": "k_predict_mc", "kernel_ms": mc_ms,
+            "achieved": ach / 1e9, "peak": PEAK_VALU_GINSTS, "unit": "G wave-instr/s",
+            "frac": ach / 1e9 / PEAK_VALU_GINSTS, "valu_insts_per_launch": insts,
+            "pmc": f"profiles/pmc_k_predict_mc.json ({mc_pmc.get('tag')})",
+            "note": "VALU issue rate = SQ_INSTS_VALU per launch (rocprofv3 PMC) / the kernel's "
+                    "live HIP-event time, against 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 "
+                    "instruction; K4 (k_predict_det) and K6 run concurrently on the other stream"}
+    else:
+        res["forecast_roofline"] = None
     res["fit_stats"] = {"n_eval_mean": float(fit.n_eval.float().mean().item()),
                         "n_eval_max": int(fit.n_eval.max().item()),
                         "map_certified": float((fit.status == 70).float().mean().item()),

@@ -74,6 +74,14 @@ def main(src, tag):
                        "WRITE_SIZE_KiB": out[kf]["WRITE_SIZE"],
                        "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE half-count)"},
                       f, indent=1)
+    if keep_fit and "SQ_INSTS_VALU" in out.get("k_predict_mc", {}):
+        # the headline's K5 instruction count (bench.py forecast_roofline:
+        # the default bench shape, 500 series, 90-day horizon)
+        d = out["k_predict_mc"]
+        with open(os.path.join(prof, "pmc_k_predict_mc.json"), "w") as f:
+            json.dump({"tag": tag, "kernel": "k_predict_mc", "n_series": 500, "horizon": 90,
+                       "SQ_INSTS_VALU": d["SQ_INSTS_VALU"], "avg_ns": d.get("avg_ns"),
+                       "SQ_WAVES": d.get("SQ_WAVES")}, f, indent=1)
     for k in ("k_fit", "k_fit_polish", "k_fit_tile", "k_polish", "k_predict_det", "k_predict_mc"):
         if k in out:
             print(k, {a: (round(b, 4) if isinstance(b, float) else b) for a, b in out[k].items()})

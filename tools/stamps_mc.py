@@ -25,4 +25,4 @@ _lib._lib.pf_debug_stamps(buf, 1)
 v = np.array(list(buf), dtype=np.float64)
 rows = max(v[9], 1)
 print(f"k_predict_mc block (0,0) wave 0: setup {v[1]-v[0]:.0f} cycles; {rows:.0f} rows; row prologue {v[2]-v[1]:.0f}; per row: "
-      f"absorb {(v[4]-v[3])/rows:.0f}  trend+noise {(v[6]-v[4])/rows:.0f} (noise {(v[6]-v[5])/rows:.0f})  select {(v[7]-v[6])/rows:.0f} cycles")
+      f"absorb {(v[4]-v[3])/rows:.0f}  normals {(v[5]-v[4])/rows:.0f}  trend samples + v {(v[6]-v[5])/rows:.0f}  select {(v[7]-v[6])/rows:.0f} cycles")
