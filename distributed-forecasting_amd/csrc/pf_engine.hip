@@ -2725,9 +2725,10 @@ int pf_predict(pf_ctx *ctx, const pf_predict_args *p, void *stream) {
     a.fr_hi = (float)(ihi - khi);
     if (a.N == 1) { a.k_lo = 0; a.fr_lo = 0.f; a.k_hi_neg = 0; a.fr_hi = 0.f; }
     // threshold selection on the normal draws of deterministic-trend rows
-    // (k_predict_mc): z* with N Phi(-z*) = k + 22 expected keys beyond it —
-    // exact whenever between k + 2 and 64 keys fall beyond (else the
-    // general selection runs): ~99% of rows at N = 1000
+    // (k_predict_mc_hist): z* with N Phi(-z*) = k + 22 expected keys beyond
+    // it — exact whenever between k + 2 and 64 keys fall beyond (else the
+    // general selection runs): ~99% of rows at N = 1000.  Random-trend rows
+    // (k_predict_mc) use the same z* on their own sample mean / sd first
     a.zthr = 0.0f;
     const int kmax = a.k_lo > a.k_hi_neg ? a.k_lo : a.k_hi_neg;
     if (a.N >= 200 && kmax + 22 <= 60 && !getenv_flag("PF_MC_GENERAL_SELECT")) {

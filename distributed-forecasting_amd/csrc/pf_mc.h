@@ -59,56 +59,127 @@ __device__ __forceinline__ void wave_sort_asc_n(float (&x)[NS]) {
   bitonic_merge_n<64>(x);
 }
 
+// inclusive prefix sum of an int across the wave
+__device__ __forceinline__ int wave_prefix_i32(int v) {
+  v += dpp_i32<PF_DPP_SHR(1)>(v);
+  v += dpp_i32<PF_DPP_SHR(2)>(v);
+  v += dpp_i32<PF_DPP_SHR(4)>(v);
+  v += dpp_i32<PF_DPP_SHR(8)>(v);
+  v += dpp_i32<PF_DPP_BCAST15, 0xA>(v);
+  v += dpp_i32<PF_DPP_BCAST31, 0xC>(v);
+  return v;
+}
+
+// NV float sums across the wave (butterflies interleaved), lane 0's value
+// broadcast: one uniform result per sum
+template <int NV>
+__device__ __forceinline__ void wave_sums_f32(float (&x)[NV]) {
+#define PF_BFLY(J) _Pragma("unroll") for (int i = 0; i < NV; ++i) x[i] += shfl_xor_f32<J>(x[i]);
+  PF_BFLY(1) PF_BFLY(2) PF_BFLY(4) PF_BFLY(8) PF_BFLY(16) PF_BFLY(32)
+#undef PF_BFLY
+#pragma unroll
+  for (int i = 0; i < NV; ++i) x[i] = readlane_f32(x[i], 0);
+}
+
 // Ranks kk[s] and kk[s] + 1 (0-indexed, ascending) of NS key sets held 16 per
 // lane: set s reads src[s >> 1 ? 1 : 0] (yhat / trend samples), negated for
 // odd s (upper tail); absent samples are NaN (ignored by fminf/fmaxf, never
-// below a threshold).  Threshold U_s = the (kk+2)-th smallest lane minimum, so
-// at least kk+2 keys are <= U_s; the keys strictly below U_s (M_s of them) are
-// compacted into LDS and sorted, and every rank >= M_s equals U_s (exact under
-// ties — trend samples without a new changepoint all equal the point trend).
-// Falls back to a bisection on the ordered bit patterns when kk + 2 > 64 or
-// more than 64 keys fall below U_s.  buf: NS * 64 floats of wave-private LDS.
+// below a threshold).  The keys strictly below a threshold U_s (M_s of them)
+// are compacted into LDS (lane-local counts, one wave prefix scan, no
+// per-key ballots) and sorted; a rank k < M_s is read off the sorted keys.
+//   1. zc > 0 (large N): U_s = mean -/+ zc sd of the set's source, so that
+//      ~k + 22 keys fall below for a normal-like law (zc = k_predict_mc's
+//      zthr); exact whenever k + 2 <= M_s <= 64 for every set, else step 2;
+//   2. U_s = the (kk+2)-th smallest lane minimum, so at least kk+2 keys are
+//      <= U_s, and every rank >= M_s equals U_s (exact under ties — trend
+//      samples without a new changepoint all equal the point trend); a
+//      bisection on the ordered bit patterns when kk + 2 > 64 or more than
+//      64 keys fall below U_s.
+// Both steps return the exact order statistics (the same bits).
+// buf: NS * 64 floats of wave-private LDS.
 template <int NS>
 __device__ __forceinline__ void wave_tail_select(const float (&v)[PF_NQ], const float (&tv)[PF_NQ],
                                                  const int (&kk)[NS], float *buf, float (&o0)[NS],
-                                                 float (&o1)[NS]) {
+                                                 float (&o1)[NS], float zc = 0.0f, int N = 0) {
   const int lane = pf_lane();
   auto src = [&](int s, int q) -> float { return (s < 2) ? v[q] : tv[q]; };
-  float lm[NS];
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    if (s & 1) {
-      float mx = -INFINITY;
-#pragma unroll
-      for (int q = 0; q < PF_NQ; ++q) mx = fmaxf(mx, src(s, q));
-      lm[s] = -mx;
-    } else {
-      float mn = INFINITY;
-#pragma unroll
-      for (int q = 0; q < PF_NQ; ++q) mn = fminf(mn, src(s, q));
-      lm[s] = mn;
-    }
-  }
-  wave_sort_asc_n(lm);
+  constexpr int NSRC = NS > 2 ? 2 : 1;
   float U[NS];
+  int M[NS], cl[NS], pre[NS];
+  for (int step = (zc > 0.0f && N > 0) ? 1 : 2; step <= 2; ++step) {
+    if (step == 1) {
+      float m[2 * NSRC];
 #pragma unroll
-  for (int s = 0; s < NS; ++s) U[s] = (kk[s] + 1 < 64) ? readlane_f32(lm[s], kk[s] + 1) : INFINITY;
-  int M[NS];
+      for (int i = 0; i < 2 * NSRC; ++i) m[i] = 0.0f;
 #pragma unroll
-  for (int s = 0; s < NS; ++s) M[s] = 0;
+      for (int q = 0; q < PF_NQ; ++q) {
 #pragma unroll
-  for (int q = 0; q < PF_NQ; ++q) {
+        for (int r = 0; r < NSRC; ++r) {
+          const float x = src(2 * r, q);
+          const bool ok = x == x;
+          m[2 * r] += ok ? x : 0.0f;
+          m[2 * r + 1] = ok ? fmaf(x, x, m[2 * r + 1]) : m[2 * r + 1];
+        }
+      }
+      wave_sums_f32(m);
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const float mean = m[2 * (s >> 1)] / (float)N;
+        const float sd = sqrtf(fmaxf(m[2 * (s >> 1) + 1] / (float)N - mean * mean, 0.0f));
+        U[s] = (s & 1) ? -(mean + zc * sd) : mean - zc * sd;
+      }
+    } else {
+      float lm[NS];
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        if (s & 1) {
+          float mx = -INFINITY;
+#pragma unroll
+          for (int q = 0; q < PF_NQ; ++q) mx = fmaxf(mx, src(s, q));
+          lm[s] = -mx;
+        } else {
+          float mn = INFINITY;
+#pragma unroll
+          for (int q = 0; q < PF_NQ; ++q) mn = fminf(mn, src(s, q));
+          lm[s] = mn;
+        }
+      }
+      wave_sort_asc_n(lm);
+#pragma unroll
+      for (int s = 0; s < NS; ++s) U[s] = (kk[s] + 1 < 64) ? readlane_f32(lm[s], kk[s] + 1) : INFINITY;
+    }
+    PF_STAMP1(10);
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      const float x = src(s, q);
-      const bool pr = (s & 1) ? (x > -U[s]) : (x < U[s]);
-      const unsigned long long m = __ballot(pr);
-      const int pos = M[s] + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-      if (pr && pos < 64) buf[s * 64 + pos] = (s & 1) ? -x : x;
-      M[s] += __popcll(m);
+      int c = 0;
+#pragma unroll
+      for (int q = 0; q < PF_NQ; ++q) {
+        const float x = src(s, q);
+        c += ((s & 1) ? (x > -U[s]) : (x < U[s])) ? 1 : 0;
+      }
+      cl[s] = c;
+      pre[s] = wave_prefix_i32(c);
+      M[s] = __builtin_amdgcn_readlane(pre[s], 63);
+    }
+    if (step == 1) {
+      bool ok = true;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) ok = ok && M[s] >= kk[s] + 2 && M[s] <= 64;
+      if (ok) break;
     }
   }
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    int w = pre[s] - cl[s];
+#pragma unroll
+    for (int q = 0; q < PF_NQ; ++q) {
+      const float x = src(s, q);
+      const bool pr = (s & 1) ? (x > -U[s]) : (x < U[s]);
+      if (pr && w < 64) buf[s * 64 + w] = (s & 1) ? -x : x;
+      w += pr ? 1 : 0;
+    }
+  }
+  PF_STAMP1(11);
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
   float c[NS];
@@ -117,6 +188,7 @@ __device__ __forceinline__ void wave_tail_select(const float (&v)[PF_NQ], const 
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
   wave_sort_asc_n(c);
+  PF_STAMP1(12);
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     const int k = kk[s];
@@ -141,17 +213,6 @@ __device__ __forceinline__ void wave_tail_select(const float (&v)[PF_NQ], const 
       }
     }
   }
-}
-
-// inclusive prefix sum of an int across the wave
-__device__ __forceinline__ int wave_prefix_i32(int v) {
-  v += dpp_i32<PF_DPP_SHR(1)>(v);
-  v += dpp_i32<PF_DPP_SHR(2)>(v);
-  v += dpp_i32<PF_DPP_SHR(4)>(v);
-  v += dpp_i32<PF_DPP_SHR(8)>(v);
-  v += dpp_i32<PF_DPP_BCAST15, 0xA>(v);
-  v += dpp_i32<PF_DPP_BCAST31, 0xC>(v);
-  return v;
 }
 
 // Deterministic-trend rows: the samples are yhat + sd z with z standard
@@ -418,6 +479,7 @@ __device__ __forceinline__ void mc_rows(const PredKArgs &a, const PredSeries &ps
       PF_STAMP1(6);
       if constexpr (TR) {
         float o0[4], o1[4];
+        // (the trend sets are tie-heavy: the moment threshold rarely fits them)
         wave_tail_select<4>(v, tv, kk4, buf, o0, o1);
         if (N == 1) { for (int s = 0; s < 4; ++s) o1[s] = o0[s]; }
         ylo = np_lerp(o0[0], o1[0], a.fr_lo);
@@ -427,7 +489,7 @@ __device__ __forceinline__ void mc_rows(const PredKArgs &a, const PredSeries &ps
       } else {
         // yhat tails only (no trend bands requested)
         float o0[2], o1[2];
-        wave_tail_select<2>(v, v, kk2, buf, o0, o1);
+        wave_tail_select<2>(v, v, kk2, buf, o0, o1, a.zthr, N);
         if (N == 1) { o1[0] = o0[0]; o1[1] = o0[1]; }
         ylo = np_lerp(o0[0], o1[0], a.fr_lo);
         yhi = np_lerp(-o1[1], -o0[1], a.fr_hi);

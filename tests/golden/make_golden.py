@@ -219,10 +219,29 @@ def c4_uncertified_fixture(tail_npz, n=2):
                         f_oracle_polished=np.array([r[3] for r in res]))
 
 
+def c3_uncertified_fixture(tail_npz):
+    """The configs[3] series (1M x 730 days, tools/bench_configs.py 4 --tail)
+    that ended without PF_ST_MAP, with the oracle's Stan endpoint and
+    polished MAP objectives: golden_c3_uncertified.npz."""
+    import sys as _sys
+    _sys.path.insert(0, os.path.join(os.path.dirname(OUT), "..", "tools"))
+    from tail_oracle import _one
+    z = np.load(tail_npz, allow_pickle=False)
+    n = len(z["index"])
+    res = [_one((4, z["ds"], z["y"][i], None)) for i in range(n)]
+    np.savez_compressed(os.path.join(OUT, "golden_c3_uncertified.npz"), ds=z["ds"], y=z["y"],
+                        index=z["index"], status_full_run=z["status"],
+                        f_oracle_stan=np.array([r[0] for r in res]),
+                        f_oracle_polished=np.array([r[3] for r in res]))
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["reference", "edge", "bench", "configs4", "stan64"]
     if which[0] == "c4tail":            # c4tail <tools/bench_configs.py --tail npz>
         c4_uncertified_fixture(which[1])
+        sys.exit(0)
+    if which[0] == "c3tail":            # c3tail <tools/bench_configs.py 4 --tail npz>
+        c3_uncertified_fixture(which[1])
         sys.exit(0)
     if "reference" in which:
         reference_fixture()
