@@ -15,7 +15,7 @@
 #define PF_CV_GMAX 512
 
 struct CvKArgs {
-  int n_series, n_rows, n_groups, window;
+  int n_series, n_rows, n_groups, window, ld_y, ld_f;
   const int32_t *group_start;
   const double *y;
   const float *yhat, *ylo, *yhi;
@@ -124,10 +124,10 @@ __global__ __launch_bounds__(64) void k_cv_metrics(CvKArgs a) {
   __shared__ double s_sum[PF_CV_MDAPE][PF_CV_GMAX];
   __shared__ int s_cnt[PF_CV_GMAX];
   const int series = blockIdx.x, lane = pf_lane();
-  const double *y = a.y + (size_t)series * a.n_rows;
-  const float *yh = a.yhat + (size_t)series * a.n_rows;
-  const float *lo = a.ylo ? a.ylo + (size_t)series * a.n_rows : nullptr;
-  const float *hi = a.yhi ? a.yhi + (size_t)series * a.n_rows : nullptr;
+  const double *y = a.y + (size_t)series * a.ld_y;
+  const float *yh = a.yhat + (size_t)series * a.ld_f;
+  const float *lo = a.ylo ? a.ylo + (size_t)series * a.ld_f : nullptr;
+  const float *hi = a.yhi ? a.yhi + (size_t)series * a.ld_f : nullptr;
   if (a.n_groups == 1 && a.window == a.n_rows) {
     cv_single_group(a, series, y, yh, lo, hi, reinterpret_cast<unsigned long long *>(&s_sum[0][0]),
                     PF_CV_MDAPE * PF_CV_GMAX, s_cnt);

@@ -2797,8 +2797,13 @@ int pf_cv_metrics(pf_ctx *ctx, const pf_cv_args *p, void *stream) {
   if (p->n_series < 0 || p->n_rows < 1 || p->n_groups < 1 || p->n_groups > PF_CV_GMAX ||
       p->window < 1)
     return set_err(ctx, "pf_cv_metrics: bad sizes (need n_rows >= 1, 1 <= n_groups <= 512, window >= 1)");
-  if (!p->group_start || !p->y || !p->yhat || !p->metrics)
+  if ((!p->group_start && p->n_groups != 1) || !p->y || !p->yhat || !p->metrics)
     return set_err(ctx, "pf_cv_metrics: NULL buffer");
+  if (p->ld_y < 0 || p->ld_f < 0 || (p->ld_y > 0 && p->ld_y < p->n_rows) ||
+      (p->ld_f > 0 && p->ld_f < p->n_rows))
+    return set_err(ctx, "pf_cv_metrics: row strides must be 0 or >= n_rows");
+  if (!p->group_start && p->window != p->n_rows)
+    return set_err(ctx, "pf_cv_metrics: group_start NULL needs window = n_rows (one group)");
   if ((p->yhat_lower == nullptr) != (p->yhat_upper == nullptr))
     return set_err(ctx, "pf_cv_metrics: yhat_lower/yhat_upper must be both set or both NULL");
   if (p->n_series == 0) return 0;
@@ -2807,6 +2812,8 @@ int pf_cv_metrics(pf_ctx *ctx, const pf_cv_args *p, void *stream) {
   a.n_rows = p->n_rows;
   a.n_groups = p->n_groups;
   a.window = p->window;
+  a.ld_y = p->ld_y > 0 ? p->ld_y : p->n_rows;
+  a.ld_f = p->ld_f > 0 ? p->ld_f : p->n_rows;
   a.group_start = p->group_start;
   a.y = p->y;
   a.yhat = p->yhat;

@@ -119,18 +119,30 @@ def insample_metrics(engine: E.Engine, y: torch.Tensor, yhat: torch.Tensor,
     metrics per series to MLflow, 02_training.py:187-192)."""
     n, T = int(y.shape[0]), int(y.shape[1])
     dev = y.device
-    yy = y.contiguous()
-    ff = yhat[:, :T].contiguous()
-    lo = yhat_lower[:, :T].contiguous() if yhat_lower is not None else None
-    hi = yhat_upper[:, :T].contiguous() if yhat_upper is not None else None
-    # built on the device (no host copy: capturable into a hipGraph)
-    gs = torch.arange(2, dtype=torch.int32, device=dev) * T
+
+    def rows(t):
+        # read in place (row stride ld) when the rows are unit-stride: no copy
+        # kernels in the step (the padded history / forecast buffers)
+        if t is None:
+            return None, 0
+        t = t[:, :T]
+        if t.stride(1) != 1 or t.stride(0) < T:
+            t = t.contiguous()
+        return t, int(t.stride(0))
+    yy, ld_y = rows(y)
+    ff, ld_f = rows(yhat)
+    lo, ld_lo = rows(yhat_lower)
+    hi, ld_hi = rows(yhat_upper)
+    if lo is not None and (ld_lo != ld_f or ld_hi != ld_f):
+        ff, lo, hi = ff.contiguous(), lo.contiguous(), hi.contiguous()
+        ld_f = T
     met = torch.empty((n, len(L.CV_METRICS)), dtype=torch.float64, device=dev)
-    a = L.PfCvArgs(n, T, 1, T, gs.data_ptr(), yy.data_ptr(), ff.data_ptr(),
+    # group_start NULL: one horizon group of every row (window = T)
+    a = L.PfCvArgs(n, T, 1, T, None, yy.data_ptr(), ff.data_ptr(),
                    lo.data_ptr() if lo is not None else None,
-                   hi.data_ptr() if hi is not None else None, met.data_ptr())
+                   hi.data_ptr() if hi is not None else None, met.data_ptr(), ld_y, ld_f)
     rc = engine.ctx.lib.pf_cv_metrics(engine.ctx.h, ctypes.byref(a),
                                       ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
     engine.ctx.check(rc, "pf_cv_metrics")
-    met._keep = (yy, ff, lo, hi, gs)
+    met._keep = (yy, ff, lo, hi)
     return met

@@ -194,7 +194,9 @@ def _device_dates(ds_ns: np.ndarray, dev) -> torch.Tensor:
     if T >= 2:
         step = int(ds_ns[1] - ds_ns[0])
         if step > 0 and int(ds_ns[-1] - ds_ns[0]) == step * (T - 1) and np.all(np.diff(ds_ns) == step):
-            return torch.arange(T, dtype=torch.int64, device=dev) * step + int(ds_ns[0])
+            # one kernel: exact int64 arithmetic, start + k * step
+            return torch.arange(int(ds_ns[0]), int(ds_ns[0]) + step * T, step, dtype=torch.int64,
+                                device=dev)
     return torch.from_numpy(ds_ns).to(dev)
 
 

@@ -300,10 +300,15 @@ enum { PF_CV_MSE = 0, PF_CV_RMSE = 1, PF_CV_MAE = 2, PF_CV_MAPE = 3, PF_CV_SMAPE
        PF_CV_COVERAGE = 5, PF_CV_MDAPE = 6, PF_CV_NMETRICS = 7 };
 typedef struct {
   int32_t n_series, n_rows, n_groups, window;
-  const int32_t *group_start;          /* [n_groups + 1], n_groups <= 512 */
-  const double *y;                     /* [n_series, n_rows] actuals       */
-  const float *yhat, *yhat_lower, *yhat_upper;   /* [n_series, n_rows]     */
+  const int32_t *group_start;          /* [n_groups + 1], n_groups <= 512;
+                                          NULL with n_groups = 1: one group of
+                                          every row (in-sample metrics)     */
+  const double *y;                     /* [n_series, ld_y] actuals         */
+  const float *yhat, *yhat_lower, *yhat_upper;   /* [n_series, ld_f]       */
   double *metrics;                     /* [n_series, PF_CV_NMETRICS]       */
+  int32_t ld_y, ld_f;                  /* row strides in elements (0: n_rows),
+                                          e.g. the padded history / forecast
+                                          buffers read in place             */
 } pf_cv_args;
 int pf_cv_metrics(pf_ctx *ctx, const pf_cv_args *args, void *stream);
 

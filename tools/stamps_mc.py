@@ -26,3 +26,5 @@ v = np.array(list(buf), dtype=np.float64)
 rows = max(v[9], 1)
 print(f"k_predict_mc block (0,0) wave 0: setup {v[1]-v[0]:.0f} cycles; {rows:.0f} rows; row prologue {v[2]-v[1]:.0f}; per row: "
       f"absorb {(v[4]-v[3])/rows:.0f}  normals {(v[5]-v[4])/rows:.0f}  trend samples + v {(v[6]-v[5])/rows:.0f}  select {(v[7]-v[6])/rows:.0f} cycles")
+print(f"  select split per row: lane minima + threshold sort {(v[10]-v[6])/rows:.0f}, compaction {(v[11]-v[10])/rows:.0f}, "
+      f"candidate sort {(v[12]-v[11])/rows:.0f}, ranks + lerp {(v[7]-v[12])/rows:.0f} cycles")
