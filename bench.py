@@ -313,6 +313,12 @@ def main():
                    "parallelism": f"dp{world} (series hash-sharded by (store, item); RCCL "
                                   f"all-gather of keys, forecasts, metrics, status)"},
         "kernels_ms": kern_avg,
+        "metrics": {"kind": "in-sample",
+                    "set": ["mse", "rmse", "mae", "mape"],
+                    "note": "per-series validation metrics computed in the timed step (K6 over the "
+                            "history rows) and, at N>1, RCCL-all-gathered with the keys; the "
+                            "reference's cross-validation metrics (02_training.py:178-188: 3 fold "
+                            "refits) are the dropin.forecast_store_items_cv and cv_on legs"},
         "launch": launch,
         "eager": {"value": total_series * args.steps / el_eager, "unit": "series/s",
                   "ms_per_step": el_eager / args.steps * 1e3,

@@ -1771,6 +1771,9 @@ __global__ __launch_bounds__(NW * 64, FitOcc<KMAX>::W) void k_fit_resume(FitKArg
   if (a0.grid_of) bind_grid<NW * 64>(a, blockIdx.x);
   fit_body<NW, KMAX, O0, O1, O2, MODE>(a, a.pass, a.o, a.warm_cap != 0);
 }
+// (The standalone polish at one workgroup per CU with 512 registers — no
+// spills — or at three with 168: configs[2] k_polish 24.9 -> 47.4 / 46.4 ms,
+// tools/polish_occ_ab.sh; the spilling two-per-CU budget stays.)
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
 __global__ __launch_bounds__(NW * 64, FitOcc<KMAX>::W) void k_polish(FitKArgs a0) {
   FitKArgs a = a0;
@@ -2140,6 +2143,8 @@ void pf_default_fit_opts(pf_fit_opts *o) {
   o->lbfgs_warmup = 60;
   o->lbfgs_warmup_evals = 90;  // also end a warm-up pass at 90 evaluations (tools/diag_warmup.py)
   o->tile_min_series = 2048;
+  o->polish_max_lag = 4;
+  o->polish_lag_ratio = 1e-2;
 }
 
 int pf_num_changepoints(int T, int n_changepoints, double changepoint_range) {

@@ -698,14 +698,16 @@ __device__ __forceinline__ bool qp_active(const FitKArgs &a, FitSmem<NW, KMAX, M
 // Lagged Hessian: after a full undamped Newton step (alpha = 1) the next QP
 // reuses the swept matrix of the previous one (warm start) instead of
 // recomputing it, as long as each lagged step shrinks the predicted
-// decrease by >= 100x (superlinear); otherwise, or after a backtracked step
+// decrease by >= 1 / pf_fit_opts.polish_lag_ratio (default 100x: measured,
+// 0.1 .. 0.5 save 5-6 % of k_polish at configs[4] but certify fewer series,
+// tools/lag_experiment.sh) at most polish_max_lag times in a row (default
+// 4); otherwise, or after a backtracked step
 // or a failed warm QP, the exact Hessian is recomputed.  A cold QP that hits
 // a non-positive pivot recomputes the Hessian with Levenberg-Marquardt
 // damping (x10 per retry).  A QP under any positive definite model predicts
 // zero decrease exactly at a KKT point, so the certificate holds either way;
 // oracle/stan_lbfgs.c:orc_polish_ex recomputes every iteration and reaches
 // the same MAP.
-#define PF_POLISH_MAXLAG 4
 #define PF_POLISH_MAXDAMP 24
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
 __device__ __forceinline__ bool polish_run(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm,
@@ -717,6 +719,7 @@ __device__ __forceinline__ bool polish_run(const FitKArgs &a, FitSmem<NW, KMAX, 
   const double c = 1.0 / sm.sig[2];
   const bool isd = (lane >= 2 && lane < 2 + S);
   n_newton = 0;
+  PF_COUNT(23);
   bool cert = false;
   bool need_h = true;
   int lag = 0, ndamp = 0;
@@ -730,6 +733,7 @@ __device__ __forceinline__ bool polish_run(const FitKArgs &a, FitSmem<NW, KMAX, 
     const bool fresh = need_h;
     if (fresh) {
       PF_STAMP(20);
+      PF_COUNT(15);
       hessian_collective<NW, KMAX, O0, O1, O2, MODE>(a, sm, x, gh, lam);
       __syncthreads();
       PF_STAMP(21);
@@ -766,6 +770,7 @@ __device__ __forceinline__ bool polish_run(const FitKArgs &a, FitSmem<NW, KMAX, 
     if (!qp_ok) {
       // warm QP failed: recompute the Hessian at the same point; cold QP
       // failed (non-positive pivot): damp the model and recompute
+      if (fresh) PF_COUNT(28); else PF_COUNT(29);
       if (fresh) {
         if (++ndamp > PF_POLISH_MAXDAMP) break;
         lam = (lam == 0.0) ? 1e-10 : lam * 10.0;
@@ -774,7 +779,8 @@ __device__ __forceinline__ bool polish_run(const FitKArgs &a, FitSmem<NW, KMAX, 
       lag = 0;
       continue;
     }
-    if (!fresh && !(fabs(dec) < 1e-2 * fabs(dec_prev))) {
+    if (!fresh && !(fabs(dec) < a.o.polish_lag_ratio * fabs(dec_prev))) {
+      PF_COUNT(30);
       // the lagged model stopped converging fast: recompute the Hessian
       need_h = true;
       lag = 0;
@@ -801,11 +807,12 @@ __device__ __forceinline__ bool polish_run(const FitKArgs &a, FitSmem<NW, KMAX, 
     }
     PF_STAMP(17);
     if (!acc) break;
+    if (alpha < 1.0) PF_COUNT(31);
     x = xn;
     f = fn;
     g = gn;
     lam = (lam < 1e-9) ? 0.0 : lam * 0.1;
-    need_h = !(alpha == 1.0 && lag < PF_POLISH_MAXLAG && lam == 0.0);
+    need_h = !(alpha == 1.0 && lag < a.o.polish_max_lag && lam == 0.0);
     lag = need_h ? 0 : lag + 1;
     dec_prev = dec;
   }

@@ -122,9 +122,16 @@ typedef struct {
   int32_t lbfgs_warmup, lbfgs_warmup_evals;
   /* engine: batches of at least tile_min_series series run the first L-BFGS
    * pass in the tiled kernel (16 series per workgroup, FP64 MFMA row pass,
-   * per-series lane-quad L-BFGS) when the layout allows it (linear / flat
-   * growth, P <= 60, K <= 32, shared prior scales); < 0 never.            */
+   * 16 lanes of L-BFGS per series) when the layout allows it (linear, flat
+   * or logistic growth, P <= 72, K <= 48, shared prior scales); < 0 never. */
   int32_t tile_min_series;
+  /* engine polish: after a full undamped Newton step the next QP reuses the
+   * swept Hessian (at most polish_max_lag times in a row) as long as each
+   * lagged QP's predicted decrease is below polish_lag_ratio times the
+   * previous one; otherwise the exact Hessian is recomputed.  Defaults 4,
+   * 1e-2.                                                                  */
+  int32_t polish_max_lag;
+  double polish_lag_ratio;
 } pf_fit_opts;
 
 /* component blocks pf_predict can report (seasonalities, holidays, ...) */

@@ -37,6 +37,8 @@ def main():
                     help="series of the Stan-faithful (stan_map) run that estimates the "
                          "algorithmic evaluation count E (0: skip)")
     ap.add_argument("--lib", default=None, help="load this engine library instead (A/B runs)")
+    ap.add_argument("--opt", action="append", default=[],
+                    help="pf_fit_opts override name=value (repeatable), e.g. polish_lag_ratio=0.1")
     args = ap.parse_args()
     if args.lib:
         from distributed_forecasting_amd import _lib
@@ -102,6 +104,9 @@ def main():
 
     def run(k):
         kw = {} if args.tile_min is None else {"tile_min_series": args.tile_min}
+        for ov in args.opt:
+            k_, v_ = ov.split("=", 1)
+            kw[k_] = float(v_) if "." in v_ or "e" in v_ else int(v_)
         fit = eng.fit(grid, Yd[k], cap=None if capd is None else capd[k], **kw)
         fg = eng.predict_grid(fit, fut)
         cf = None
@@ -187,7 +192,7 @@ def main():
     stats = [(ne.double().mean().item(), (st == 70).double().mean().item()) for ne, st, _, _ in stats]
     res = {"metric": "series fit+forecast/sec", "config_index": args.config, "value": n / el,
            "unit": "series/s", "n_gpus": 1, "seconds": el, "workload": work, "chunk": chunk,
-           "kernels_ms_total": kern, "tile_min_series": args.tile_min,
+           "kernels_ms_total": kern, "tile_min_series": args.tile_min, "opt": args.opt,
            "n_eval_mean": float(np.mean([s[0] for s in stats])),
            "map_certified": float(np.mean([s[1] for s in stats])),
            "roofline": roof, "uncertified": tail,

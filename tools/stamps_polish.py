@@ -8,7 +8,7 @@ import ctypes, os, sys
 import numpy as np, torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from distributed_forecasting_amd import _lib
-_lib.load(os.path.abspath("distributed-forecasting_amd/libprophet_hip_stamps.so"))
+_lib.load(os.path.abspath(os.environ.get("PF_STAMPS_LIB", "distributed-forecasting_amd/libprophet_hip_stamps.so")))
 import distributed_forecasting_amd as dfa
 from distributed_forecasting_amd import synthetic, holidays as H
 from distributed_forecasting_amd.engine import ProphetConfig
@@ -45,9 +45,10 @@ for i in range(n):
     eng.ctx.set_timing(False)
     _lib._lib.pf_debug_stamps(buf, 1)
     v = np.array(list(buf), dtype=np.float64)
-    rows.append(dict(newton=v[18], sweeps=v[26], qp_it=v[27], hess=v[21] - v[20], sweep_in=v[24] - v[21],
+    rows.append(dict(hessians=v[15], polish_calls=v[23], damped=v[28], warm_qp_fail=v[29], lag_reject=v[30], backtracked=v[31], newton=v[18], sweeps=v[26], qp_it=v[27], hess=v[21] - v[20], sweep_in=v[24] - v[21],
                      qp=v[22] - v[19], armijo=v[17] - v[16], n_eval=int(fit.n_eval[0]),
                      status=int(fit.status[0]), kernels={k: round(x, 3) for k, x in kt.items()}))
     print(rows[-1], flush=True)
-m = {k: float(np.mean([r[k] for r in rows])) for k in ("newton", "sweeps", "qp_it", "hess", "sweep_in", "qp", "armijo")}
+m = {k: float(np.mean([r[k] for r in rows])) for k in ("hessians", "polish_calls", "damped", "warm_qp_fail", "lag_reject", "backtracked", "newton", "sweeps", "qp_it", "hess", "sweep_in", "qp", "armijo")}
 print("mean", {k: round(x) for k, x in m.items()})
+print("cycles per Hessian", round(sum(r["hess"] for r in rows) / max(1, sum(r["hessians"] for r in rows))))
