@@ -71,7 +71,7 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=500,
                     help="series in the CPU-baseline sample (0 disables)")
     ap.add_argument("--cpu-workers", type=int, default=0, help="0: min(16, cpu_count)")
-    ap.add_argument("--dropin-steps", type=int, default=3)
+    ap.add_argument("--dropin-steps", type=int, default=10)
     ap.add_argument("--c2-steps", type=int, default=3)
     ap.add_argument("--c2-series", type=int, default=C2_SERIES)
     ap.add_argument("--no-variants", action="store_true",
@@ -491,7 +491,7 @@ def dropin(args, eng, keys, ds, Y, Yd, rank, world, bracket, max_over_ranks, sum
                 g = parallel.gather_results(kt, None, mt)
                 met = g["metrics"]
         return fr, met
-    el, ka, (fr, _) = timed(fsi, steps)
+    el, ka, (fr, _) = timed(fsi, steps, warm=2)
     out["forecast_store_items"] = {
         "value": tot * steps / el, "unit": "series/s", "ms_per_call": el / steps * 1e3,
         "rows_out": int(len(fr)),
@@ -500,7 +500,7 @@ def dropin(args, eng, keys, ds, Y, Yd, rank, world, bracket, max_over_ranks, sum
                 "[ds, store, item, y, yhat, yhat_upper, yhat_lower] frame out (float32, int32 "
                 "keys); grouping, grid bucketing, H2D/D2H and frame assembly included; N>1: "
                 "this rank's hash shard + tensor all-gather of the frames"}
-    el, ka, (fr, met) = timed(lambda: fsi(True), steps)
+    el, ka, (fr, met) = timed(lambda: fsi(True), steps, warm=2)
     out["forecast_store_items_cv"] = {
         "value": tot * steps / el, "unit": "series/s", "ms_per_call": el / steps * 1e3,
         "kernels_ms": ka,
@@ -520,7 +520,7 @@ def dropin(args, eng, keys, ds, Y, Yd, rank, world, bracket, max_over_ranks, sum
         inp = pd.DataFrame({"ds": np.tile(futd.astype("datetime64[ns]"), n),
                             "store": np.repeat(keys[:, 0], len(futd)).astype(np.int32),
                             "item": np.repeat(keys[:, 1], len(futd)).astype(np.int32)})
-        el, ka, _ = timed(lambda: model.predict(None, inp), steps)
+        el, ka, _ = timed(lambda: model.predict(None, inp), steps, warm=2)
         out["pyfunc_predict"] = {
             "value": tot * steps / el, "unit": "series/s", "ms_per_call": el / steps * 1e3,
             "note": "ForecastStoreItemModel.predict(context, model_input) (model_wrapper.py:43-73) "
