@@ -60,6 +60,31 @@ def test_ragged_fit_and_forecast_equal_per_bucket():
     assert np.all(rb.fit.status.cpu().numpy() == 70)
 
 
+def test_ragged_sample_mode_equal_per_bucket():
+    """interval_method='sample' (every row's 1000 samples; the history rows
+    in k_predict_mc_hist, the horizon in k_predict_mc, both binding each
+    series' own grid): one ragged launch == one launch per bucket, bit for
+    bit, with and without trend bands."""
+    cfg = ProphetConfig.reference()
+    cfg.interval_method = "sample"
+    e = dfa.Engine(0, cfg)
+    df, gkeys, bks = _buckets()
+    pkeys = np.concatenate([gkeys[bk.members] for bk in bks])
+    rb = B.RaggedFittedBatch.fit_buckets(e, bks, series_ids=B.series_id(pkeys))
+    futs = rb.future(90, "D")
+    for comp in (False, True):
+        _, out = rb.predict(futs, seed=5, components=comp)
+        torch.cuda.synchronize()
+        for j, bk in enumerate(bks):
+            r0, r1 = int(rb.row0[j]), int(rb.row0[j + 1])
+            fb = B.FittedBatch.fit_dense(e, bk.fit_ds, bk.Y, history_dates=bk.history_dates,
+                                         series_ids=B.series_id(pkeys[r0:r1]))
+            Tf, o1 = fb.predict(futs[j], seed=5, components=comp)
+            keys = ("yhat", "yhat_lower", "yhat_upper") + (("trend_lower", "trend_upper") if comp else ())
+            for k in keys:
+                assert torch.equal(o1[k][:, :Tf], out[k][r0:r1, :Tf]), (comp, j, k)
+
+
 def test_ragged_matches_oracle():
     """Per series on its own grid: objective <= oracle Stan + 1e-6 (rel),
     equal to the oracle's certified MAP within 1e-9, yhat within
