@@ -206,7 +206,7 @@ def main():
         out = eng.predict(fit, fg, seed=0, components=False, series_id=sid,
                           interval_method=method)
         met = diagnostics.insample_metrics(eng, Yd[:, :T], out["yhat"], out["yhat_lower"],
-                                           out["yhat_upper"])
+                                           out["yhat_upper"], mdape=False)
         if world > 1:
             blk = torch.stack([out["yhat"], out["yhat_lower"], out["yhat_upper"]], 1)
             parallel.gather_results(kd, blk, met[:, :4].contiguous(), fit.status, counts=counts)
@@ -316,7 +316,9 @@ def main():
         "metrics": {"kind": "in-sample",
                     "set": ["mse", "rmse", "mae", "mape"],
                     "note": "per-series validation metrics computed in the timed step (K6 over the "
-                            "history rows) and, at N>1, RCCL-all-gathered with the keys; the "
+                            "history rows: mse, rmse, mae, mape, smape, coverage; the MDAPE median "
+                            "is not computed — the reference logs mse / mae / mape) and, at N>1, "
+                            "RCCL-all-gathered with the keys; the "
                             "reference's cross-validation metrics (02_training.py:178-188: 3 fold "
                             "refits) are the dropin.forecast_store_items_cv and cv_on legs"},
         "launch": launch,
@@ -575,7 +577,7 @@ def configs2(args, eng, ds, seasons, fut, rank, world, device, timed, sum_over_r
         fg = eng.predict_grid(fit, fut)
         out = eng.predict(fit, fg, seed=0, components=False, series_id=sid)
         met = diagnostics.insample_metrics(eng, Yd[:, :T], out["yhat"], out["yhat_lower"],
-                                           out["yhat_upper"])
+                                           out["yhat_upper"], mdape=False)
         if world > 1:
             import torch
             blk = torch.stack([out["yhat"], out["yhat_lower"], out["yhat_upper"]], 1)

@@ -80,7 +80,8 @@ class PfPredictArgs(ctypes.Structure):
 class PfCvArgs(ctypes.Structure):
     _fields_ = [("n_series", i32), ("n_rows", i32), ("n_groups", i32), ("window", i32),
                 ("group_start", vp), ("y", vp), ("yhat", vp), ("yhat_lower", vp),
-                ("yhat_upper", vp), ("metrics", vp), ("ld_y", i32), ("ld_f", i32)]
+                ("yhat_upper", vp), ("metrics", vp), ("ld_y", i32), ("ld_f", i32),
+                ("skip_mdape", i32)]
 
 
 class PfKernelTime(ctypes.Structure):

@@ -15,7 +15,7 @@
 #define PF_CV_GMAX 512
 
 struct CvKArgs {
-  int n_series, n_rows, n_groups, window, ld_y, ld_f;
+  int n_series, n_rows, n_groups, window, ld_y, ld_f, skip_mdape;
   const int32_t *group_start;
   const double *y;
   const float *yhat, *ylo, *yhi;
@@ -95,14 +95,16 @@ __device__ __forceinline__ void cv_single_group(const CvKArgs &a, int series, co
   for (int o = 32; o >= 1; o >>= 1) ymin = fmin(ymin, __shfl_xor(ymin, o, 64));
   bool bad = false;
   const bool cached = n <= ncache;
-  for (int r = lane; r < n; r += 64) {
-    const double v = fabs((y[r] - (double)yh[r]) / y[r]);
-    bad |= (v != v);
-    if (cached) cache[r] = (unsigned long long)__double_as_longlong(v);
+  if (!a.skip_mdape) {
+    for (int r = lane; r < n; r += 64) {
+      const double v = fabs((y[r] - (double)yh[r]) / y[r]);
+      bad |= (v != v);
+      if (cached) cache[r] = (unsigned long long)__double_as_longlong(v);
+    }
   }
   const bool anybad = __ballot(bad) != 0ull;
   double v0 = NAN, v1 = NAN;
-  if (!anybad) {
+  if (!anybad && !a.skip_mdape) {
     v0 = cv_radix_select(cached ? cache : nullptr, n, (n - 1) / 2, y, yh, hist);
     v1 = (n % 2) ? v0 : cv_radix_select(cached ? cache : nullptr, n, n / 2, y, yh, hist);
   }
@@ -116,7 +118,7 @@ __device__ __forceinline__ void cv_single_group(const CvKArgs &a, int series, co
     m[PF_CV_MAPE] = (full && ymin >= 1e-8) ? ape / w : NAN;
     m[PF_CV_SMAPE] = full ? sape / w : NAN;
     m[PF_CV_COVERAGE] = (full && lo) ? cov / w : NAN;
-    m[PF_CV_MDAPE] = (a.window <= n && !anybad) ? (v0 + v1) * 0.5 : NAN;
+    m[PF_CV_MDAPE] = (a.window <= n && !anybad && !a.skip_mdape) ? (v0 + v1) * 0.5 : NAN;
   }
 }
 
@@ -163,7 +165,9 @@ __global__ __launch_bounds__(64) void k_cv_metrics(CvKArgs a) {
   // sorted by horizon) until the window is filled; a group is kept iff
   // rows up to its end >= window (monotone: UPSTREAM's backward sweep stops
   // at the first group that cannot fill it).  Median by rank counting.
-  {
+  if (a.skip_mdape) {
+    if (lane == 0) a.metrics[(size_t)series * PF_CV_NMETRICS + PF_CV_MDAPE] = NAN;
+  } else {
     double macc = 0.0, mcnt = 0.0;
     for (int g = lane; g < a.n_groups; g += 64) {
       const int gs = a.group_start[g], r1 = a.group_start[g + 1];

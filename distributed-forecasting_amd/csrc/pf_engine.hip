@@ -2819,6 +2819,7 @@ int pf_cv_metrics(pf_ctx *ctx, const pf_cv_args *p, void *stream) {
   a.window = p->window;
   a.ld_y = p->ld_y > 0 ? p->ld_y : p->n_rows;
   a.ld_f = p->ld_f > 0 ? p->ld_f : p->n_rows;
+  a.skip_mdape = p->skip_mdape ? 1 : 0;
   a.group_start = p->group_start;
   a.y = p->y;
   a.yhat = p->yhat;

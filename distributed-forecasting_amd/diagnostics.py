@@ -110,13 +110,14 @@ def cv_metrics_batch(engine: E.Engine, fit_ds, Y, **kw) -> dict:
 
 def insample_metrics(engine: E.Engine, y: torch.Tensor, yhat: torch.Tensor,
                      yhat_lower: torch.Tensor | None = None,
-                     yhat_upper: torch.Tensor | None = None) -> torch.Tensor:
+                     yhat_upper: torch.Tensor | None = None, mdape: bool = True) -> torch.Tensor:
     """[n, 7] float64 device tensor of K6's metric set over the history rows
     (one horizon group, window = every row: the plain means, the median for
     MDAPE; MAPE NaN where UPSTREAM skips it).  ``y`` [n, T] float64 and
     ``yhat`` [n, >= T] float32 on the device; the per-series validation
     metrics the multi-GPU path all-gathers (the reference logs its CV
-    metrics per series to MLflow, 02_training.py:187-192)."""
+    metrics per series to MLflow, 02_training.py:187-192).  ``mdape=False``
+    skips the median (NaN): the reference logs mse / mae / mape only."""
     n, T = int(y.shape[0]), int(y.shape[1])
     dev = y.device
 
@@ -140,7 +141,8 @@ def insample_metrics(engine: E.Engine, y: torch.Tensor, yhat: torch.Tensor,
     # group_start NULL: one horizon group of every row (window = T)
     a = L.PfCvArgs(n, T, 1, T, None, yy.data_ptr(), ff.data_ptr(),
                    lo.data_ptr() if lo is not None else None,
-                   hi.data_ptr() if hi is not None else None, met.data_ptr(), ld_y, ld_f)
+                   hi.data_ptr() if hi is not None else None, met.data_ptr(), ld_y, ld_f,
+                   0 if mdape else 1)
     rc = engine.ctx.lib.pf_cv_metrics(engine.ctx.h, ctypes.byref(a),
                                       ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
     engine.ctx.check(rc, "pf_cv_metrics")

@@ -37,7 +37,7 @@ class ForecastStep:
 
     def __init__(self, engine: E.Engine, ds_ns: np.ndarray, n: int, *, horizon: int = 90,
                  freq_ns: int = E.NS_PER_DAY, series_id: torch.Tensor | None = None,
-                 seed: int = 0, metrics: bool = True, interval_method: str | None = None,
+                 seed: int = 0, metrics: bool | str = True, interval_method: str | None = None,
                  components: bool = False):
         if E.Context._by_device.get(engine.device) is engine.ctx:
             engine = E.Engine(engine.device, engine.config, own_context=True)
@@ -92,8 +92,12 @@ class ForecastStep:
             cur.wait_stream(self.mc_stream)     # K5 writes the history rows' intervals too
         if self.metrics:
             # exact intervals: the history rows are written by K4 on this stream
+            # the per-series validation metrics the reference logs (mse /
+            # mae / mape, 02_training.py:187-192) and rmse, smape, coverage;
+            # the MDAPE median is skipped (NaN) unless metrics="all"
             res["metrics"] = diagnostics.insample_metrics(
-                eng, self.Y[:, :self.T], out["yhat"], out["yhat_lower"], out["yhat_upper"])
+                eng, self.Y[:, :self.T], out["yhat"], out["yhat_lower"], out["yhat_upper"],
+                mdape=self.metrics == "all")
         cur.wait_stream(self.mc_stream)
         return res
 

@@ -316,6 +316,8 @@ typedef struct {
   int32_t ld_y, ld_f;                  /* row strides in elements (0: n_rows),
                                           e.g. the padded history / forecast
                                           buffers read in place             */
+  int32_t skip_mdape;                  /* 1: MDAPE not computed (NaN): the
+                                          reference logs mse / mae / mape    */
 } pf_cv_args;
 int pf_cv_metrics(pf_ctx *ctx, const pf_cv_args *args, void *stream);
 
