@@ -79,3 +79,40 @@ def test_tile_flat_growth_and_short_grid():
     assert np.all(ft.status.cpu().numpy() == fs.status.cpu().numpy())
     f_t, f_s = ft.f.cpu().numpy(), fs.f.cpu().numpy()
     assert np.all(np.abs(f_t - f_s) <= 1e-9 * np.abs(f_s))
+
+
+def test_tile_default_size_matches_per_series():
+    """at the size where K3T runs by default (n = 4096 >=
+    tile_min_series = 2048, configs[2]'s generator, the persistent schedule
+    with slot refills): the default fit (warm-up hand-off to the polish)
+    certifies the same MAP as Stan's full run + polish (fit_mode stan_map)
+    on all but a measured <= 0.1 % of series — the warm-up hand-off can
+    certify a neighbouring local optimum (1 of 4096 here, 4.6e-4 relative;
+    tools/diag_tile_basin.py) — for the tiled and the per-series
+    first pass alike; where both reach stan_map's MAP their forecasts agree
+    within 1e-6 y_scale; refits are bitwise reproducible."""
+    n = 4096
+    e, g, ds, Y, Yd = _setup(n)
+    ft = e.fit(g, Yd)                       # default: tiled first pass
+    ft2 = e.fit(g, Yd)
+    fs = e.fit(g, Yd, tile_min_series=-1)   # per-series kernel
+    fm = e.fit(g, Yd, stan_faithful=True, tile_min_series=-1)
+    f_m = fm.f.cpu().numpy()
+    ok = {}
+    for name, fit in (("tile", ft), ("series", fs)):
+        st = fit.status.cpu().numpy()
+        assert np.mean(st == 70) >= 0.999, (name, np.unique(st, return_counts=True))
+        rel = (fit.f.cpu().numpy() - f_m) / np.abs(f_m)
+        assert np.mean(rel > 1e-9) <= 1e-3, (name, int(np.sum(rel > 1e-9)))
+        assert rel.max() < 1e-3, (name, float(rel.max()))
+        ok[name] = (np.abs(rel) <= 1e-9) & (st == 70)
+    assert torch.equal(ft.theta, ft2.theta) and torch.equal(ft.f, ft2.f)
+    both = ok["tile"] & ok["series"]
+    fut = np.concatenate([ds, ds[-1] + synthetic.NS_PER_DAY * np.arange(1, 91)])
+    fg = e.predict_grid(ft, fut)
+    sid = torch.arange(n, dtype=torch.int32, device="cuda")
+    ot = e.predict(ft, fg, seed=0, components=False, series_id=sid)
+    os_ = e.predict(fs, fg, seed=0, components=False, series_id=sid)
+    ys = ft.y_scale.cpu().numpy()[:, None]
+    d = np.abs(ot["yhat"][:, :fg.T].double().cpu().numpy() - os_["yhat"][:, :fg.T].double().cpu().numpy()) / ys
+    assert np.all(d[both] <= 1e-6), float(d[both].max())
