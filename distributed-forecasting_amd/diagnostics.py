@@ -63,6 +63,48 @@ def cv_metrics_device(engine: E.Engine, fit_ds: np.ndarray, Y, *, horizon_days: 
         seasons = engine.config.seasons(int(fit_ds[0]), int(fit_ds[-1]),
                                         B.min_positive_diff(fit_ds))
     y_parts, f_parts, lo_parts, hi_parts, h_parts = [], [], [], [], []
+    folds = []
+    for c in cutoffs:
+        tr = fit_ds <= c
+        if int(tr.sum()) < 2:
+            raise ValueError("Less than two datapoints before cutoff. Increase initial window.")
+        folds.append((c, int(tr.sum()), np.flatnonzero((fit_ds > c) & (fit_ds <= c + horizon))))
+    sids = None
+    if series_ids is not None:
+        sids = torch.from_numpy(np.ascontiguousarray(series_ids, dtype=np.int32)).to(dev)
+    packed = (priors is None and len(folds) > 1 and engine.config.growth != "logistic" and
+              n * len(folds) < engine.fit_opts().tile_min_series)
+    if packed:
+        # every fold's refit and forecast in ONE launch per kernel: the folds
+        # are the sub-grids of a ragged batch (same seasonalities, each with
+        # its own changepoints on its truncated history, UPSTREAM
+        # prophet_copy), bitwise the per-fold launches (tests/test_gpu_ragged.py)
+        # while the folds' slow series overlap instead of each launch
+        # waiting for its own slowest series
+        cfg = engine.config
+        Tp = E.pad_rows(max(k for _, k, _ in folds))
+        G = len(folds)
+        rg = E.RaggedGrid.build([fit_ds[:k] for _, k, _ in folds], seasons,
+                                [int(fit_ds[0])] * G, [int(fit_ds[k - 1] - fit_ds[0]) for _, k, _ in folds],
+                                np.repeat(np.arange(G), n), device=engine.device, T_pad=Tp,
+                                n_changepoints=cfg.n_changepoints,
+                                changepoint_range=cfg.changepoint_range)
+        Yp = torch.zeros((G * n, Tp), dtype=torch.float64, device=dev)
+        for g, (_, k, _) in enumerate(folds):
+            Yp[g * n:(g + 1) * n, :k] = Yt[:, :k]
+        fit = engine.fit(rg, Yp)
+        fg = engine.predict_grid(fit, [fit_ds[te] for _, _, te in folds])
+        out = engine.predict(fit, fg, n_samples=None if coverage else 0, seed=seed,
+                             components=False,
+                             series_id=sids.repeat(G) if sids is not None else None)
+        for g, (c, k, te) in enumerate(folds):
+            Tf = len(te)
+            y_parts.append(Yt[:, te[0]:te[-1] + 1] if np.all(np.diff(te) == 1) else Yt[:, te])
+            f_parts.append(out["yhat"][g * n:(g + 1) * n, :Tf])
+            lo_parts.append(out["yhat_lower"][g * n:(g + 1) * n, :Tf])
+            hi_parts.append(out["yhat_upper"][g * n:(g + 1) * n, :Tf])
+            h_parts.append(fit_ds[te] - c)
+        cutoffs = []
     for c in cutoffs:
         tr = fit_ds <= c
         if int(tr.sum()) < 2:
