@@ -155,7 +155,7 @@ __device__ __forceinline__ float pf_ppnd16f(float p, float q) {
 // Gamma(alpha, 1), integer-valued alpha >= 1, single precision: Exp(1) by
 // inversion when alpha == 1, Marsaglia–Tsang otherwise (one Philox block
 // per two proposals: Box–Muller pair + two acceptance uniforms)
-__device__ __noinline__ float pf_gamma_f(float alpha, pf_rowrng &rng) {
+__device__ __forceinline__ float pf_gamma_f(float alpha, pf_rowrng &rng) {
   if (alpha <= 1.0f) {
     const pf_u4 r = rng.next();
     return -logf(pf_u01f(r.x));
