@@ -284,9 +284,13 @@ __device__ __forceinline__ double pf_u01d(uint32_t a, uint32_t b) {
   return ((double)(v & ((1ull << 53) - 1)) + 0.5) * (1.0 / 9007199254740992.0);
 }
 
-// Box-Muller: two normals from two uniforms (v_sin/v_cos take revolutions)
+// Box-Muller: two normals from two uniforms (v_sin/v_cos take revolutions).
+// -2 ln u1 = -2 ln2 log2 u1 on the hardware log2 and sqrt (v_log_f32,
+// v_sqrt_f32, ~1 ulp): pf_u01f's uniforms are >= 2^-25, never denormal, so
+// the library forms' denormal scaling and ln2 extension (~17 instructions
+// per pair) buy nothing here.
 __device__ __forceinline__ void pf_box_muller(float u1, float u2, float &z0, float &z1) {
-  const float r = __fsqrt_rn(-2.0f * __logf(u1));
+  const float r = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));
   z0 = r * __builtin_amdgcn_cosf(u2);
   z1 = r * __builtin_amdgcn_sinf(u2);
 }
