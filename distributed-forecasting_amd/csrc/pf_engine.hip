@@ -219,6 +219,7 @@ __device__ void grid_changepoints(const double *__restrict__ t, int T, int n_cp_
     cp_idx[0] = -1;
   }
 }
+#define PF_GRID_CP_LDS 4096  // changepoints k_grid_segments places in LDS (32 KB)
 __global__ void k_grid_changepoints(const double *__restrict__ t, int T, int n_cp_req, double range,
                                     double *__restrict__ t_change, int32_t *__restrict__ cp_idx) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
@@ -259,10 +260,52 @@ __device__ __forceinline__ void grid_segments(int i, const double *__restrict__ 
     cp_first[i] = lo;
   }
 }
-__global__ void k_grid_segments(const double *__restrict__ t, int T, int Tp,
-                                const double *__restrict__ t_change, int S,
-                                int32_t *__restrict__ seg, int32_t *__restrict__ cp_first) {
-  grid_segments(blockIdx.x * blockDim.x + threadIdx.x, t, T, Tp, t_change, S, seg, cp_first);
+// With n_cp_req >= 0 every block first places the changepoints itself (the
+// rule of grid_changepoints, one index per thread, then the same stable
+// insertion sort, in LDS) and block 0 writes t_change / cp_idx: one launch
+// instead of a single-thread k_grid_changepoints (~12 us of serial loads on
+// the headline step's critical path) followed by this one.  Bitwise the
+// two-kernel form.  n_cp_req < 0: t_change is the caller's (read only).
+__global__ __launch_bounds__(256) void k_grid_segments(const double *__restrict__ t, int T, int Tp,
+                                                       double *__restrict__ t_change, int S,
+                                                       int n_cp_req, double range,
+                                                       int32_t *__restrict__ cp_idx,
+                                                       int32_t *__restrict__ seg,
+                                                       int32_t *__restrict__ cp_first) {
+  extern __shared__ double s_tc[];
+  const double *tc = t_change;
+  if (n_cp_req >= 0) {
+    const int hist_size = (int)floor((double)T * range);
+    int n_cp = n_cp_req;
+    if (n_cp + 1 > hist_size) n_cp = hist_size - 1;
+    if (n_cp > 0) {
+      const double stop = (double)(hist_size - 1);
+      const double step = stop / (double)n_cp;
+      for (int j = 1 + (int)threadIdx.x; j <= n_cp; j += blockDim.x) {
+        const double v = (j == n_cp) ? stop : __dmul_rn((double)j, step);
+        const int idx = (int)rint(v);
+        if (blockIdx.x == 0) cp_idx[j - 1] = idx;
+        s_tc[j - 1] = t[idx];
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        for (int a = 1; a < n_cp; ++a) {
+          double v = s_tc[a];
+          int b = a - 1;
+          while (b >= 0 && s_tc[b] > v) { s_tc[b + 1] = s_tc[b]; --b; }
+          s_tc[b + 1] = v;
+        }
+      }
+    } else if (threadIdx.x == 0) {
+      s_tc[0] = 0.0;  // dummy changepoint, S = 1
+      if (blockIdx.x == 0) cp_idx[0] = -1;
+    }
+    __syncthreads();
+    if (blockIdx.x == 0)
+      for (int j = threadIdx.x; j < S; j += blockDim.x) t_change[j] = s_tc[j];
+    tc = s_tc;
+  }
+  grid_segments(blockIdx.x * blockDim.x + threadIdx.x, t, T, Tp, tc, S, seg, cp_first);
 }
 // ragged: grid g = blockIdx.y; also writes grid g's pf_grid descriptor
 __global__ void k_grids_segments(const int64_t *__restrict__ prm, int Tp, int K, int S,
@@ -2176,18 +2219,24 @@ int pf_build_grid(pf_ctx *ctx, const int64_t *ds_ns, int T, int T_pad, int64_t s
   PF_TIMED_LAUNCH(ctx, "k_grid_features", nb, st, k_grid_features, dim3(nb), dim3(256), 0, st,
                   ds_ns, T, T_pad, start_ns, t_scale_ns, ss, extra_cols, n_extra, t_out, XT_out);
   PF_HIP(ctx, hipGetLastError());
+  // changepoints placed inside k_grid_segments while they fit in LDS
+  const bool fused_cp = n_changepoints >= 0 && S <= PF_GRID_CP_LDS;
   if (n_changepoints >= 0) {
     if (!cp_idx_out) return set_err(ctx, "pf_build_grid: cp_idx_out NULL");
     const int n_expect = pf_num_changepoints(T, n_changepoints, changepoint_range);
     if ((n_expect > 0 ? n_expect : 1) != S)
       return set_err(ctx, "pf_build_grid: S does not match pf_num_changepoints");
-    PF_TIMED_LAUNCH(ctx, "k_grid_changepoints", 1, st, k_grid_changepoints, dim3(1), dim3(64), 0,
-                    st, t_out, T, n_changepoints, changepoint_range, t_change_io, cp_idx_out);
-    PF_HIP(ctx, hipGetLastError());
+    if (!fused_cp) {
+      PF_TIMED_LAUNCH(ctx, "k_grid_changepoints", 1, st, k_grid_changepoints, dim3(1), dim3(64), 0,
+                      st, t_out, T, n_changepoints, changepoint_range, t_change_io, cp_idx_out);
+      PF_HIP(ctx, hipGetLastError());
+    }
   }
   const int ns = ((T_pad > S ? T_pad : S) + 255) / 256;
-  PF_TIMED_LAUNCH(ctx, "k_grid_segments", ns, st, k_grid_segments, dim3(ns), dim3(256), 0, st,
-                  t_out, T, T_pad, t_change_io, S, seg_out, cp_first_out);
+  PF_TIMED_LAUNCH(ctx, "k_grid_segments", ns, st, k_grid_segments, dim3(ns), dim3(256),
+                  fused_cp ? (size_t)S * sizeof(double) : 0, st, t_out, T, T_pad, t_change_io, S,
+                  fused_cp ? n_changepoints : -1, changepoint_range,
+                  fused_cp ? cp_idx_out : nullptr, seg_out, cp_first_out);
   PF_HIP(ctx, hipGetLastError());
   return 0;
 }
