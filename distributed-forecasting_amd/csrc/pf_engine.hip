@@ -355,11 +355,29 @@ __global__ __launch_bounds__(256) void k_prepare(int T, int Tp, const double *__
   }
   const double *ys = y + (size_t)s * Tp;
   double amax = 0.0, vmin = INFINITY, vmax = -INFINITY, vsum = 0.0;
-  for (int i = threadIdx.x; i < T; i += blockDim.x) {
-    const double v = ys[i];
-    amax = fmax(amax, fabs(v));
-    vmin = fmin(vmin, v);
-    vmax = fmax(vmax, v);
+  // rows up to PF_PREP_REG * 256 stay in registers between the two passes
+  // (one read of y instead of two)
+  constexpr int PF_PREP_REG = 8;
+  const bool in_reg = Tp <= PF_PREP_REG * 256;
+  double yr[PF_PREP_REG];
+  if (in_reg) {
+#pragma unroll
+    for (int k = 0; k < PF_PREP_REG; ++k) {
+      const int i = threadIdx.x + k * 256;
+      yr[k] = i < T ? ys[i] : 0.0;
+      if (i < T) {
+        amax = fmax(amax, fabs(yr[k]));
+        vmin = fmin(vmin, yr[k]);
+        vmax = fmax(vmax, yr[k]);
+      }
+    }
+  } else {
+    for (int i = threadIdx.x; i < T; i += blockDim.x) {
+      const double v = ys[i];
+      amax = fmax(amax, fabs(v));
+      vmin = fmin(vmin, v);
+      vmax = fmax(vmax, v);
+    }
   }
   for (int o = 32; o >= 1; o >>= 1) {
     amax = fmax(amax, __shfl_xor(amax, o, 64));
@@ -374,10 +392,22 @@ __global__ __launch_bounds__(256) void k_prepare(int T, int Tp, const double *__
   vmax = fmax(fmax(red[2][0], red[2][1]), fmax(red[2][2], red[2][3]));
   double scale = amax == 0.0 ? 1.0 : amax;
   double *out = y_scaled + (size_t)s * Tp;
-  for (int i = threadIdx.x; i < Tp; i += blockDim.x) {
-    const double v = (i < T) ? ys[i] / scale : 0.0;
-    out[i] = v;
-    if (i < T) vsum += v;
+  if (in_reg) {
+#pragma unroll
+    for (int k = 0; k < PF_PREP_REG; ++k) {
+      const int i = threadIdx.x + k * 256;
+      if (i < Tp) {
+        const double v = (i < T) ? yr[k] / scale : 0.0;
+        out[i] = v;
+        if (i < T) vsum += v;
+      }
+    }
+  } else {
+    for (int i = threadIdx.x; i < Tp; i += blockDim.x) {
+      const double v = (i < T) ? ys[i] / scale : 0.0;
+      out[i] = v;
+      if (i < T) vsum += v;
+    }
   }
   if (growth == PF_GROWTH_LOGISTIC) {
     // UPSTREAM initialize_scales: cap_scaled = (cap - floor) / y_scale, floor 0
@@ -2318,7 +2348,10 @@ int pf_prepare(pf_ctx *ctx, int n_series, const pf_grid *grid, int growth, const
 // Position q = r*NL + L of the copy holds natural row i = L*R + r (rows past
 // T: t = 0, X = 0, seg = S, no changepoint starts).  Built per fit call into
 // the context workspace (K+1 doubles + 1 int per position; ~0.4 MB at 1826
-// days), read by every series of the batch.
+// days), read by every series of the batch.  One column per blockIdx.y, so
+// the copy spreads over (K + 1) x ceil(TQ / 256) workgroups rather than
+// ceil(TQ / 256) threads each walking the K strided columns (11 -> ~4 us at
+// 1826 days; the copy sits on the fit's critical path).
 __global__ __launch_bounds__(256) void k_permute_grid(const double *__restrict__ t,
                                                       const int32_t *__restrict__ seg,
                                                       const double *__restrict__ XT, int T, int Tp,
@@ -2332,11 +2365,15 @@ __global__ __launch_bounds__(256) void k_permute_grid(const double *__restrict__
   const int r = q / NL, L = q - r * NL;
   const int i = L * R + r;
   const bool v = i < T;
-  tP[q] = v ? t[i] : 0.0;
-  const int sg = v ? seg[i] : S;
-  const int sp = v ? (i > 0 ? seg[i - 1] : 0) : S;
-  sgP[q] = sg | ((sg - sp) << 16);
-  for (int f = 0; f < K; ++f) XTP[(size_t)f * TQ + q] = v ? XT[(size_t)f * Tp + i] : 0.0;
+  const int f = (int)blockIdx.y - 1;  // y = 0: t and seg; y = f + 1: column f
+  if (f < 0) {
+    tP[q] = v ? t[i] : 0.0;
+    const int sg = v ? seg[i] : S;
+    const int sp = v ? (i > 0 ? seg[i - 1] : 0) : S;
+    sgP[q] = sg | ((sg - sp) << 16);
+  } else {
+    XTP[(size_t)f * TQ + q] = v ? XT[(size_t)f * Tp + i] : 0.0;
+  }
 }
 
 // Ragged batch: the lane-blocked copy of every grid (blockIdx.y = grid), each
@@ -2344,7 +2381,7 @@ __global__ __launch_bounds__(256) void k_permute_grid(const double *__restrict__
 __global__ __launch_bounds__(256) void k_permute_grid_ragged(const pf_grid *__restrict__ grids,
                                                              int Tp, int K, int S, int NL,
                                                              char *__restrict__ base, size_t stride) {
-  const int g = blockIdx.y;
+  const int g = blockIdx.y;  // blockIdx.z: which column, as in k_permute_grid
   const int T = __builtin_amdgcn_readfirstlane(grids[g].T);
   const int R = (T + NL - 1) / NL, TQ = NL * R;
   const int q = blockIdx.x * 256 + threadIdx.x;
@@ -2358,11 +2395,15 @@ __global__ __launch_bounds__(256) void k_permute_grid_ragged(const pf_grid *__re
   const int r = q / NL, L = q - r * NL;
   const int i = L * R + r;
   const bool v = i < T;
-  tP[q] = v ? t[i] : 0.0;
-  const int sg = v ? seg[i] : S;
-  const int sp = v ? (i > 0 ? seg[i - 1] : 0) : S;
-  sgP[q] = sg | ((sg - sp) << 16);
-  for (int f = 0; f < K; ++f) XTP[(size_t)f * TQ + q] = v ? XT[(size_t)f * Tp + i] : 0.0;
+  const int f = (int)blockIdx.z - 1;  // z = 0: t and seg; z = f + 1: column f
+  if (f < 0) {
+    tP[q] = v ? t[i] : 0.0;
+    const int sg = v ? seg[i] : S;
+    const int sp = v ? (i > 0 ? seg[i - 1] : 0) : S;
+    sgP[q] = sg | ((sg - sp) << 16);
+  } else {
+    XTP[(size_t)f * TQ + q] = v ? XT[(size_t)f * Tp + i] : 0.0;
+  }
 }
 
 // Row-major feature copy for K3T: XR[r][f] = X[r][f] (f < K), 0 for K <= f < W
@@ -2591,8 +2632,8 @@ static int prepare_fit_scratch(pf_ctx *ctx, FitKArgs &a, hipStream_t st, bool ro
     a.sgP = nullptr;
     a.XR = nullptr;
     const int nb = (int)((TQ + 255) / 256);
-    PF_TIMED_LAUNCH(ctx, "k_permute_grid_ragged", nb * n_grids, st, k_permute_grid_ragged,
-                    dim3(nb, n_grids), dim3(256), 0, st, a.grids, a.Tp, a.K, a.S, PF_FIT_NW * 64,
+    PF_TIMED_LAUNCH(ctx, "k_permute_grid_ragged", nb * n_grids * (a.K + 1), st,
+                    k_permute_grid_ragged, dim3(nb, n_grids, a.K + 1), dim3(256), 0, st, a.grids, a.Tp, a.K, a.S, PF_FIT_NW * 64,
                     (char *)w, gbytes);
     PF_HIP(ctx, hipGetLastError());
     return 0;
@@ -2609,7 +2650,8 @@ static int prepare_fit_scratch(pf_ctx *ctx, FitKArgs &a, hipStream_t st, bool ro
   a.XR = nullptr;
   a.XR_width = 0;
   const int nb = (int)((TQ + 255) / 256);
-  PF_TIMED_LAUNCH(ctx, "k_permute_grid", nb, st, k_permute_grid, dim3(nb), dim3(256), 0, st,
+  PF_TIMED_LAUNCH(ctx, "k_permute_grid", nb * (a.K + 1), st, k_permute_grid, dim3(nb, a.K + 1),
+                  dim3(256), 0, st,
                   a.t, a.seg, a.XT, a.T, a.Tp, a.K, a.S, a.R, PF_FIT_NW * 64,
                   const_cast<double *>(a.tP), const_cast<int32_t *>(a.sgP),
                   const_cast<double *>(a.XTP));
