@@ -70,7 +70,12 @@ def parse():
     ap.add_argument("--series-per-gpu", type=int, default=SERIES_PER_GPU)
     ap.add_argument("--cpu-sample", type=int, default=500,
                     help="series in the CPU-baseline sample (0 disables)")
-    ap.add_argument("--cpu-workers", type=int, default=0, help="0: min(16, cpu_count)")
+    ap.add_argument("--cpu-workers", type=int, default=0,
+                    help="0: every CPU this process may use (cpu_share())")
+    ap.add_argument("--cpu-cv-sample", type=int, default=128,
+                    help="series in the CV-on CPU-baseline sample (0 disables)")
+    ap.add_argument("--gather", choices=("rank0", "all"), default="rank0",
+                    help="N>1 exchange: gather to rank 0 (the frame's consumer) or all-gather")
     ap.add_argument("--dropin-steps", type=int, default=10)
     ap.add_argument("--c2-steps", type=int, default=3)
     ap.add_argument("--c2-series", type=int, default=C2_SERIES)
@@ -126,6 +131,75 @@ def _cpu_extra(args):
     return yh[0], yh[1], st.hist.y_scale
 
 
+def _cpu_one_cv(args):
+    """One series with the reference's train_model CV (02_training.py:178-188):
+    3 fold refits (UPSTREAM cross_validation: horizon 90 d, period 360 d,
+    initial 730 d), each fold's 90-row forecast with 1000-sample intervals,
+    performance_metrics + the notebook's mean over horizons; then the full
+    fit + 90-day forecast with intervals (as _cpu_one)."""
+    ds, y, seed = args
+    from oracle import prophet_oracle as po, stan_oracle as so
+    rng = np.random.default_rng(seed)
+    H = HORIZON * po.NS_PER_DAY
+    cut = po.generate_cutoffs(ds, H, 730 * po.NS_PER_DAY, 360 * po.NS_PER_DAY)
+    ys, fs, hs = [], [], []
+    for c in cut:
+        tr = ds <= c
+        te = (ds > c) & (ds <= c + H)
+        st = po.build_problem(ds[tr], y[tr])
+        th = so.fit_setup(st)[0]
+        o = po.sample_uncertainty(st, po.params_from_theta(th, st.problem.S), ds[te],
+                                  n_samples=N_SAMPLES, rng=rng)
+        ys.append(y[te]); fs.append(o["yhat"]); hs.append(ds[te] - c)
+    pm = po.performance_metrics(np.concatenate(ys), np.concatenate(fs), np.concatenate(hs),
+                                metrics=("mse", "mae", "mape"))
+    met = {m: float(np.mean(pm[m])) for m in ("mse", "mae", "mape") if m in pm}
+    yh, th = _cpu_one((ds, y, seed + 1))
+    return met, yh
+
+
+def cpu_share():
+    """CPUs this process may use: the affinity mask, capped by a cgroup CPU
+    quota and by OMP_NUM_THREADS when the environment sets them (on the GPU
+    box os.cpu_count() reports the whole machine, not this job's share)."""
+    info = {"os_cpu_count": os.cpu_count()}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        info["affinity"] = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    info["cgroup_quota"] = quota
+    omp = os.environ.get("OMP_NUM_THREADS")
+    info["omp_num_threads"] = int(omp) if omp and omp.isdigit() else None
+    n = info["affinity"]
+    if quota:
+        n = min(n, max(1, int(quota)))
+    if info["omp_num_threads"]:
+        n = min(n, info["omp_num_threads"])
+    info["usable"] = n
+    return info
+
+
+def cpu_baseline_cv(ds, Y, n_sample: int, workers: int):
+    import multiprocessing as mp
+    jobs = [(ds, Y[i], 5000 + 7 * i) for i in range(n_sample)]
+    ctx = mp.get_context("fork")
+    with ctx.Pool(workers) as pool:
+        pool.map(_cpu_one, [(ds, Y[i], 1) for i in range(workers)])
+        t0 = time.perf_counter()
+        res = pool.map(_cpu_one_cv, jobs, chunksize=1)
+        dt = time.perf_counter() - t0
+    return dict(rate=n_sample / dt, dt=dt, n=n_sample,
+                metric_means={k: float(np.nanmean([r[0][k] for r in res])) for k in res[0][0]})
+
+
 def cpu_baseline(ds, Y, n_sample: int, workers: int):
     import multiprocessing as mp
     from oracle import stan_oracle as so
@@ -163,11 +237,15 @@ def main():
     # CPU baseline first (rank 0, N=1): forked workers, before the GPU is touched
     cpu = None
     if world == 1 and rank == 0 and args.cpu_sample > 0:
-        workers = args.cpu_workers or min(16, os.cpu_count() or 1)
+        share = cpu_share()
+        workers = args.cpu_workers or share["usable"]
         n_s = min(max(args.cpu_sample, workers), len(keys))
         cpu = cpu_baseline(ds, Y_all, n_s, workers)
         cpu["n"] = n_s
         cpu["workers"] = workers
+        cpu["share"] = share
+        if args.cpu_cv_sample > 0:
+            cpu["cv"] = cpu_baseline_cv(ds, Y_all, min(args.cpu_cv_sample, len(keys)), workers)
 
     import torch
     import torch.distributed as dist
@@ -209,7 +287,7 @@ def main():
                                            out["yhat_upper"], mdape=False)
         if world > 1:
             blk = torch.stack([out["yhat"], out["yhat_lower"], out["yhat_upper"]], 1)
-            parallel.gather_results(kd, blk, met[:, :4].contiguous(), fit.status, counts=counts)
+            parallel.gather_results(kd, blk, met[:, :4].contiguous(), fit.status, counts=counts, dst=dst)
         return fit, fg, out, met
 
     def bracket():
@@ -243,19 +321,25 @@ def main():
             k[1] += 1
         return {k: v[0] / v[1] for k, v in kern.items()}
 
-    def timed(fn, steps, warm=1, ctx=None):
+    def timed(fn, steps, warm=1, ctx=None, drain=None):
         """Same bracketing as the headline: warm-up, barrier + sync, `steps`
         calls, barrier + sync, max over ranks; kernel averages from the HIP
-        events of the engine context the launches go through."""
+        events of the engine context the launches go through.  ``drain``
+        completes work still in flight (asynchronous exchanges) inside the
+        timed region."""
         ctx = ctx or eng.ctx
         for _ in range(warm):
             fn()
+        if drain:
+            drain()
         bracket()
         ctx.set_timing(True)
         t0_ = time.perf_counter()
         r = None
         for _ in range(steps):
             r = fn()
+        if drain:
+            drain()
         bracket()
         el = time.perf_counter() - t0_
         ka = averages(ctx.read_timings())
@@ -267,26 +351,50 @@ def main():
     # runs on every replay; the host-side launch work is recorded once), the
     # RCCL gather after the replay; the eager launches are timed first (their
     # HIP events give the per-kernel times the roofline uses)
-    fstep = dfa.ForecastStep(eng, ds, n, horizon=HORIZON, series_id=sid)
+    fstep = dfa.ForecastStep(eng, ds, n, horizon=HORIZON, series_id=sid, metrics="fast")
     fstep.set_inputs(Yd[:, :T])
 
     def unpack(r):
         return r["fit"], r["forecast_grid"], r["forecast"], r["metrics"]
 
+    dst = 0 if args.gather == "rank0" else None
+    pending = []
+    xbytes = {}
+
     def gather(r):
+        # the exchange runs asynchronously on RCCL's stream: the copies below
+        # snapshot this step's outputs (the replayed graph rewrites its static
+        # buffers), so step k's gather overlaps step k+1's kernels
         if world > 1:
             o = r["forecast"]
             blk = torch.stack([o["yhat"], o["yhat_lower"], o["yhat_upper"]], 1)
-            parallel.gather_results(kd, blk, r["metrics"][:, :4].contiguous(), r["fit"].status,
-                                    counts=counts)
+            g = parallel.gather_results(kd, blk, r["metrics"][:, :4].contiguous(),
+                                        r["fit"].status.clone(), counts=counts, dst=dst,
+                                        async_op=True)
+            pending.append(g)
+            xbytes.update(g["bytes"])
         return r
 
+    def drain():
+        while pending:
+            pending.pop(0).wait()
+
+    def stepped(fn):
+        def run():
+            r = fn()
+            if len(pending) > 2:            # bound the in-flight exchanges
+                pending.pop(0).wait()
+            return r
+        return run
+
     sctx = fstep.engine.ctx                 # the step's private context (graphs.py)
-    el_eager, kern_avg, _ = timed(lambda: gather(fstep.run()), args.steps, args.warmup, sctx)
+    el_eager, kern_avg, _ = timed(stepped(lambda: gather(fstep.run())), args.steps, args.warmup,
+                                  sctx, drain=drain)
     launch = "hipGraph replay"
     try:
         fstep.capture()
-        elapsed, _, r = timed(lambda: gather(fstep.replay()), args.steps, args.warmup, sctx)
+        elapsed, _, r = timed(stepped(lambda: gather(fstep.replay())), args.steps, args.warmup,
+                              sctx, drain=drain)
     except Exception as e:                  # capture unsupported: report the eager step
         launch = f"eager (graph capture failed: {type(e).__name__}: {e})"
         elapsed, r = el_eager, fstep.run()
@@ -327,6 +435,26 @@ def main():
                   "note": "the same step launched eagerly (Python + ctypes per launch); "
                           "kernels_ms and the roofline come from these launches' HIP events"},
     }
+
+    # ------------------------------------------------------ exchange bytes
+    # per series: int64 keys (16 B), the [3, T_pad] fp32 forecast block,
+    # 4 fp64 metrics, int32 status; projected for the 8-GPU weak-scaling run
+    # (500 series per GPU, splitmix64 shards padded to the largest rank)
+    row_b = 16 + 3 * int(out["yhat"].shape[1]) * 4 + 4 * 8 + 4
+    k8 = keys_for(8 * args.series_per_gpu)
+    mx8 = int(np.bincount(B.shard_of(k8, 8), minlength=8).max())
+    proj8 = 7 * mx8 * row_b
+    link_gbs = 64.0        # assumed sustained one-direction xGMI rate per peer link (GB/s)
+    res["exchange"] = {
+        "mode": ("gather to rank 0" if dst == 0 else "all-gather") +
+                " (RCCL, asynchronous: overlaps the next step's kernels)",
+        "bytes_per_step_this_rank": xbytes if world > 1 else {"sent": 0, "received": 0},
+        "bytes_per_series": row_b,
+        "projected_n8": {"max_rank_series": mx8, "rank0_received_bytes_per_step": proj8,
+                         "other_rank_sent_bytes_per_step": mx8 * row_b,
+                         "projected_ms_at_7_links": proj8 / (7 * link_gbs * 1e9) * 1e3,
+                         "assumed_link_GBps": link_gbs,
+                         "note": "all-gather: every rank receives the rank-0 figure"}}
 
     # ---------------------------------------------------------- roofline
     with open(os.path.join(ROOT, "tests", "golden", "bench_manifest.json")) as f:
@@ -436,12 +564,23 @@ def main():
                     "L-BFGS stops (the reference-shaped answer).  Stan's endpoint itself moves "
                     "by the last line's amount when its init is perturbed by 1e-14 (its "
                     "termination at the |delta| kink is rounding-sensitive)."}
+        cv = cpu.get("cv")
         res["cpu_baseline"] = {
             "value": cpu["rate"], "unit": "series/s", "cores": cpu["workers"], "kind": "port",
             "sample": (f"all {m} bench series; per series: Stan L-BFGS MAP (oracle C "
                        f"restatement) + 90-day forecast with {N_SAMPLES}-sample intervals (numpy "
-                       f"restatement); {cpu['workers']}-process pool, {cpu['dt']:.1f} s wall; "
-                       f"CV off (the reference's train_model adds 3 CV refits)")}
+                       f"restatement); {cpu['workers']}-process pool (Spark local[{cpu['workers']}] "
+                       f"shape: one series per task), {cpu['dt']:.1f} s wall; CV off"),
+            "cpu_share": cpu["share"],
+            "cv_on": None if cv is None else {
+                "value": cv["rate"], "unit": "series/s", "cores": cpu["workers"], "n_series": cv["n"],
+                "wall_s": cv["dt"], "cv_metric_means": cv["metric_means"],
+                "sample": (f"first {cv['n']} bench series; per series the reference's train_model: "
+                           f"3 CV fold refits (1016/1376/1736 rows) each with a 90-row "
+                           f"{N_SAMPLES}-sample forecast + performance_metrics (mse/mae/mape), then "
+                           f"the full fit + 90-day forecast with intervals (02_training.py:172-205)")},
+            "note": ("cores = the CPUs this process may use (affinity, capped by the cgroup quota "
+                     "and OMP_NUM_THREADS: the box's share; os_cpu_count is the whole machine)")}
     else:
         res["cpu_baseline"] = None
     if rank == 0:

@@ -22,7 +22,7 @@ PF_ST_CONSTANT = 50
 EXPORTED = ["pf_ctx_create", "pf_ctx_destroy", "pf_last_error", "pf_default_fit_opts",
             "pf_num_changepoints", "pf_build_grid", "pf_prepare", "pf_objective_grad",
             "pf_fit", "pf_predict", "pf_set_timing", "pf_read_timings", "pf_cv_metrics",
-            "pf_hessian", "pf_prepare_ragged", "pf_build_grids"]
+            "pf_hessian", "pf_prepare_ragged", "pf_build_grids", "pf_build_id"]
 PF_MAX_COMP = 32  # include/prophet_hip.h
 PF_INTERVAL = {"exact": 0, "sample": 1}
 PF_PREDICT_DET, PF_PREDICT_MC = 1, 2
@@ -91,8 +91,25 @@ class PfKernelTime(ctypes.Structure):
 _lib = None
 
 
+def check_build_id(path: str = LIB_PATH, csrc: str | None = None, include: str | None = None) -> str:
+    """Refuse a library that was not compiled from the sources next to it:
+    its embedded PF_BUILD_ID must equal the hash of csrc/ + include/ (build.py).
+    Returns the id.  Raises EngineUnavailable on a mismatch (a stale .so)."""
+    from . import build as _build
+    src = _build.source_hash(csrc or _build.CSRC, include or _build.INCLUDE)
+    got = _build.embedded_id(path)
+    if src is None:
+        raise EngineUnavailable(f"engine sources not found next to {path}: cannot verify the build")
+    if got != src:
+        raise EngineUnavailable(
+            f"{path} is stale: built from sources with id {got}, the sources on disk hash to "
+            f"{src}; rebuild with `python -c 'import __graft_entry__ as g; g.build()'`")
+    return got
+
+
 def load(path: str = LIB_PATH):
-    """Load the HIP engine library (raises EngineUnavailable if absent)."""
+    """Load the HIP engine library (raises EngineUnavailable if absent, or if
+    the in-tree library's build id does not match its sources)."""
     global _lib
     if _lib is not None:
         return _lib
@@ -100,6 +117,8 @@ def load(path: str = LIB_PATH):
         raise EngineUnavailable(
             f"{path} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
             " (hipcc --offload-arch=gfx950). There is no CPU fallback.")
+    if os.path.abspath(path) == LIB_PATH:
+        check_build_id(path)
     try:
         lib = ctypes.CDLL(path)
     except OSError as e:  # pragma: no cover - depends on the ROCm runtime
@@ -108,6 +127,8 @@ def load(path: str = LIB_PATH):
     lib.pf_ctx_destroy.argtypes = [vp]
     lib.pf_last_error.argtypes = [vp]
     lib.pf_last_error.restype = ctypes.c_char_p
+    lib.pf_build_id.argtypes = []
+    lib.pf_build_id.restype = ctypes.c_char_p
     lib.pf_default_fit_opts.argtypes = [ctypes.POINTER(PfFitOpts)]
     lib.pf_default_fit_opts.restype = None
     lib.pf_num_changepoints.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double]
@@ -131,7 +152,7 @@ def load(path: str = LIB_PATH):
     lib.pf_set_timing.argtypes = [vp, ctypes.c_int]
     lib.pf_read_timings.argtypes = [vp, ctypes.POINTER(PfKernelTime), ctypes.c_int]
     for name in EXPORTED:
-        if name not in ("pf_default_fit_opts",):
+        if name not in ("pf_default_fit_opts", "pf_build_id"):
             getattr(lib, name).restype = getattr(lib, name).restype or ctypes.c_int
     _lib = lib
     return lib

@@ -1,38 +1,78 @@
-"""Build the gfx950 engine library in-tree (hipcc, no cmake)."""
+"""Build the gfx950 engine library in-tree (hipcc, no cmake).
+
+The library carries a build id: a SHA-256 over every file under csrc/ and
+include/ plus the compile flags, baked in as ``PF_BUILD_ID`` and returned by
+``pf_build_id()``.  ``build()`` recompiles whenever the id embedded in the
+existing .so differs from the id of the sources on disk (not on mtimes: a
+pushed tree may carry a prebuilt .so with any timestamp), and ``_lib.load()``
+refuses a library whose id does not match the sources next to it.
+"""
 from __future__ import annotations
 
+import hashlib
 import os
+import re
 import subprocess
 import sys
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _ROOT = os.path.dirname(_HERE)
-SOURCES = [os.path.join(_HERE, "csrc", "pf_engine.hip")]
-DEPS = SOURCES + [os.path.join(_HERE, "csrc", "pf_common.h"),
-                  os.path.join(_HERE, "csrc", "pf_polish.h"),
-                  os.path.join(_HERE, "csrc", "pf_cv.h"),
-                  os.path.join(_HERE, "csrc", "pf_ostat.h"),
-                  os.path.join(_HERE, "csrc", "pf_mc.h"),
-                  os.path.join(_HERE, "csrc", "pf_tile.h"),
-                  os.path.join(_ROOT, "include", "prophet_hip.h")]
+CSRC = os.path.join(_HERE, "csrc")
+INCLUDE = os.path.join(_ROOT, "include")
+SOURCES = [os.path.join(CSRC, "pf_engine.hip")]
 OUT = os.path.join(_HERE, "libprophet_hip.so")
 ARCH = os.environ.get("PF_OFFLOAD_ARCH", "gfx950")
+FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared"]
+_ID_RE = re.compile(rb"PF_BUILD_ID:([0-9a-f]{32})")
+
+
+def source_files(csrc: str = CSRC, include: str = INCLUDE) -> list:
+    """Every file the library is compiled from (sorted, absolute)."""
+    out = []
+    for d in (csrc, include):
+        if os.path.isdir(d):
+            out += [os.path.join(d, f) for f in sorted(os.listdir(d))
+                    if f.endswith((".h", ".hip", ".hpp"))]
+    return out
+
+
+def source_hash(csrc: str = CSRC, include: str = INCLUDE) -> str | None:
+    """Build id of the sources on disk (None when they are absent)."""
+    files = source_files(csrc, include)
+    if not files:
+        return None
+    h = hashlib.sha256()
+    h.update(" ".join(FLAGS).encode())
+    for p in files:
+        h.update(b"\0" + os.path.basename(p).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:32]
+
+
+def embedded_id(so_path: str = OUT) -> str | None:
+    """The build id baked into a built library (read from its bytes: no
+    dlopen, so it works without a GPU runtime)."""
+    if not os.path.exists(so_path):
+        return None
+    with open(so_path, "rb") as f:
+        m = _ID_RE.search(f.read())
+    return m.group(1).decode() if m else None
 
 
 def needs_build() -> bool:
     if not os.path.exists(OUT):
         return True
-    t = os.path.getmtime(OUT)
-    return any(os.path.getmtime(d) > t for d in DEPS if os.path.exists(d))
+    return embedded_id(OUT) != source_hash()
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
     if not force and not needs_build():
         return OUT
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-I", os.path.join(_ROOT, "include"), "-I", os.path.join(_HERE, "csrc"),
-           "-o", OUT + ".tmp", *SOURCES]
+    bid = source_hash()
+    cmd = [hipcc, *FLAGS, f'-DPF_BUILD_ID="{bid}"',
+           "-I", INCLUDE, "-I", CSRC, "-o", OUT + ".tmp", *SOURCES]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)

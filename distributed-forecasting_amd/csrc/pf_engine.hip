@@ -2236,6 +2236,14 @@ static int ctx_workspace(pf_ctx *ctx, size_t bytes, void **out) {
 
 const char *pf_last_error(pf_ctx *ctx) { return ctx ? ctx->err : g_err_noctx; }
 
+// build id: SHA-256 (32 hex digits) of csrc/ + include/ + the compile flags,
+// passed by build.py; _lib.load() compares it with the sources on disk
+#ifndef PF_BUILD_ID
+#define PF_BUILD_ID "unversioned"
+#endif
+static const char pf_build_id_str[] = "PF_BUILD_ID:" PF_BUILD_ID;
+const char *pf_build_id(void) { return pf_build_id_str + 12; }
+
 void pf_default_fit_opts(pf_fit_opts *o) {
   o->init_alpha = 1e-3;
   o->tol_obj = 1e-12;

@@ -48,9 +48,13 @@ def generate_cutoffs(ds_ns, horizon_ns: int, initial_ns: int, period_ns: int) ->
 def cv_metrics_device(engine: E.Engine, fit_ds: np.ndarray, Y, *, horizon_days: float = 90,
                       period_days: float = 360, initial_days: float = 730,
                       rolling_window: float = 0.1, seasons=None, coverage: bool = False,
-                      seed: int = 0, series_ids=None, priors=None) -> torch.Tensor:
-    """[n, 6] float64 device tensor: mse, rmse, mae, mape, smape, coverage
-    (each the mean over horizons of the rolled metric) for every row of Y."""
+                      seed: int = 0, series_ids=None, priors=None,
+                      packed: bool | None = None) -> torch.Tensor:
+    """[n, 7] float64 device tensor: mse, rmse, mae, mape, smape, coverage,
+    mdape (each the mean over horizons of the rolled metric) for every row of
+    Y.  ``packed``: None picks the launch shape (every fold in one ragged
+    launch while the batch is below the tiled path's size, else one launch
+    per fold); True / False force it (the two are bitwise equal)."""
     fit_ds = np.asarray(fit_ds, np.int64)
     dev = torch.device("cuda", engine.device)
     Yt = Y if isinstance(Y, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(Y, np.float64))
@@ -72,8 +76,11 @@ def cv_metrics_device(engine: E.Engine, fit_ds: np.ndarray, Y, *, horizon_days: 
     sids = None
     if series_ids is not None:
         sids = torch.from_numpy(np.ascontiguousarray(series_ids, dtype=np.int32)).to(dev)
-    packed = (priors is None and len(folds) > 1 and engine.config.growth != "logistic" and
-              n * len(folds) < engine.fit_opts().tile_min_series)
+    can_pack = priors is None and len(folds) > 1 and engine.config.growth != "logistic"
+    if packed is None:
+        packed = can_pack and n * len(folds) < engine.fit_opts().tile_min_series
+    elif packed and not can_pack:
+        raise ValueError("packed folds need shared priors, >1 fold and non-logistic growth")
     if packed:
         # every fold's refit and forecast in ONE launch per kernel: the folds
         # are the sub-grids of a ragged batch (same seasonalities, each with

@@ -15,6 +15,7 @@ Mapping to the reference:
 from __future__ import annotations
 
 import ctypes
+import weakref
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -108,6 +109,9 @@ class ProphetConfig:
 # context (one per device)
 # ---------------------------------------------------------------------------
 class Context:
+    """One pf_ctx (its fit workspace and timing events).  ``close()`` (or
+    garbage collection) calls pf_ctx_destroy; the per-device shared contexts
+    of ``get`` live for the process."""
     _by_device: dict = {}
 
     def __init__(self, device: int):
@@ -118,6 +122,27 @@ class Context:
         if rc != 0:
             raise RuntimeError(f"pf_ctx_create failed: {self.lib.pf_last_error(None).decode()}")
         self.h = h
+        self._fin = weakref.finalize(self, Context._destroy, self.lib, h.value)
+        self._fin.atexit = False       # process teardown releases the device anyway
+
+    @staticmethod
+    def _destroy(lib, handle):
+        lib.pf_ctx_destroy(ctypes.c_void_p(handle))
+
+    @property
+    def closed(self) -> bool:
+        return not self._fin.alive
+
+    def close(self) -> None:
+        """Destroy the C context now (hipFree of its workspace).  Callers must
+        not have work in flight that uses it (graphs replaying it, launches on
+        other streams): synchronise first.  The shared per-device contexts are
+        never closed this way."""
+        if Context._by_device.get(self.device) is self:
+            raise RuntimeError("the shared per-device context is not closed by callers")
+        if self._fin.alive:
+            self._fin()
+        self.h = ctypes.c_void_p(0)
 
     @classmethod
     def get(cls, device: int) -> "Context":
@@ -483,9 +508,16 @@ class Engine:
         fits of this engine may run concurrently with another engine's on
         other streams (e.g. two ForecastSteps replayed in a pipeline)."""
         self.device = device
+        self.owns_context = bool(own_context)
         self.ctx = Context(device) if own_context else Context.get(device)
         self.config = config or ProphetConfig.reference()
         self._vec_cache = {}
+
+    def close(self) -> None:
+        """Release a private context (own_context=True); no-op for the shared one."""
+        if self.owns_context and not self.ctx.closed:
+            torch.cuda.synchronize(self.device)
+            self.ctx.close()
 
     # prior scales and mode indicators (UPSTREAM regressor_column_matrix)
     def _vectors(self, grid: DeviceGrid):
@@ -650,7 +682,7 @@ class Engine:
 
     def fit(self, grid: DeviceGrid, Y: torch.Tensor, polish: bool | None = None,
             stan_faithful: bool | None = None, cap: torch.Tensor | None = None, priors=None,
-            **opt) -> FitResult:
+            init=None, **opt) -> FitResult:
         """Fit every row of Y [n, T_pad] (raw y, float64, on this GPU).
 
         ``polish`` / ``stan_faithful`` default to the config's ``fit_mode``:
@@ -668,6 +700,8 @@ class Engine:
             stan_faithful = mode == "stan_map"
         n = Y.shape[0]
         y_scale, y_scaled, theta, status, cap_scaled = self.prepare(grid, Y, cap)
+        if init is not None:
+            init(theta)
         dev = Y.device
         f = torch.empty(n, dtype=torch.float64, device=dev)
         f_stan = torch.empty(n, dtype=torch.float64, device=dev)

@@ -16,8 +16,15 @@ The captured kernels keep pointers into that workspace (the fit's grid
 copies), so a step never shares it: when the engine given uses the
 per-device shared context, the step runs on a private engine (same config,
 its own C-ABI context) — a later, larger fit elsewhere cannot reallocate
-the buffers a graph replays on.  RCCL collectives stay outside the graph
-(run them after replay).
+the buffers a graph replays on.  A step that made its private engine owns
+it: ``close()`` (or garbage collection of the step) drops the graph first and
+then destroys that context (pf_ctx_destroy).  RCCL collectives stay outside
+the graph (run them after replay).
+
+``metrics``: True (default) computes the whole in-sample set K6 offers
+(mse, rmse, mae, mape, smape, coverage and the MDAPE median); "fast" skips
+the MDAPE median (NaN) — the set the reference logs (mse / mae / mape,
+02_training.py:187-192) plus rmse, smape, coverage; False: no metrics.
 """
 from __future__ import annotations
 
@@ -39,8 +46,12 @@ class ForecastStep:
                  freq_ns: int = E.NS_PER_DAY, series_id: torch.Tensor | None = None,
                  seed: int = 0, metrics: bool | str = True, interval_method: str | None = None,
                  components: bool = False):
+        if metrics not in (True, False, "fast", "all"):
+            raise ValueError("metrics must be True, False or 'fast'")
+        self._owns_engine = False
         if E.Context._by_device.get(engine.device) is engine.ctx:
             engine = E.Engine(engine.device, engine.config, own_context=True)
+            self._owns_engine = True
         self.engine = engine
         cfg = engine.config
         self.ds = np.asarray(ds_ns, np.int64)
@@ -94,10 +105,10 @@ class ForecastStep:
             # exact intervals: the history rows are written by K4 on this stream
             # the per-series validation metrics the reference logs (mse /
             # mae / mape, 02_training.py:187-192) and rmse, smape, coverage;
-            # the MDAPE median is skipped (NaN) unless metrics="all"
+            # the MDAPE median unless metrics="fast"
             res["metrics"] = diagnostics.insample_metrics(
                 eng, self.Y[:, :self.T], out["yhat"], out["yhat_lower"], out["yhat_upper"],
-                mdape=self.metrics == "all")
+                mdape=self.metrics != "fast")
         cur.wait_stream(self.mc_stream)
         return res
 
@@ -129,3 +140,20 @@ class ForecastStep:
             raise RuntimeError("capture() first")
         self.graph.replay()
         return self.out
+
+    def close(self) -> None:
+        """Drop the captured graph and the outputs, then destroy the private
+        context this step created (a caller-given private engine is left to
+        its owner)."""
+        if self.graph is not None or self.out is not None:
+            torch.cuda.synchronize(self.Y.device)
+        self.graph = None
+        self.out = None
+        if self._owns_engine:
+            self.engine.close()
+
+    def __enter__(self) -> "ForecastStep":
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.close()

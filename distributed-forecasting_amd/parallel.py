@@ -39,39 +39,105 @@ def gather_counts(n_local: int, device) -> list:
     return [int(c) for c in cn.tolist()]
 
 
-def gather_blocks(local: torch.Tensor, counts=None):
-    """All-gather a per-rank [n_r, ...] block (padded to max n_r) over the
-    default process group (RCCL on GPUs, gloo on CPU).  Returns (the
-    concatenation of every rank's valid rows, in rank order, per-rank counts)."""
+class Gathered(dict):
+    """Result of ``gather_results``: keys / forecast / metrics / status (the
+    concatenation of every rank's rows in rank order; on ranks other than
+    ``dst`` only "counts" and "bytes" when gathering to one rank), "counts",
+    and "bytes" = {"sent", "received"} of this rank's share of the exchange.
+    With ``async_op=True`` the collectives are in flight: ``wait()`` before
+    reading the tensors."""
+
+    def __init__(self):
+        super().__init__()
+        self._pending = []
+
+    def wait(self) -> "Gathered":
+        for work, finish in self._pending:
+            if work is not None:
+                work.wait()
+            finish()
+        self._pending = []
+        return self
+
+
+def gather_blocks(local: torch.Tensor, counts=None, dst: int | None = None,
+                  async_op: bool = False, _into: Gathered | None = None, _key: str | None = None):
+    """Gather a per-rank [n_r, ...] block (padded to max n_r) over the default
+    process group (RCCL on GPUs, gloo on CPU): to every rank (``dst=None``,
+    all_gather_into_tensor) or to rank ``dst`` only (``dist.gather``).
+    Returns (the concatenation of every rank's valid rows in rank order —
+    None on ranks other than dst —, per-rank counts, bytes dict)."""
     ws = dist.get_world_size()
+    rank = dist.get_rank()
     if counts is None:
         counts = gather_counts(local.shape[0], local.device)
     mx = max(counts)
+    rb = int(np.prod(local.shape[1:], dtype=np.int64)) * local.element_size()
+    if mx == 0:                       # every rank knows: nothing to exchange
+        empty = local.new_empty((0,) + tuple(local.shape[1:]))
+        if dst is not None and rank != dst:
+            empty = None
+        if _into is not None and empty is not None:
+            _into[_key] = empty
+        return empty, counts, {"sent": 0, "received": 0}
     pad = torch.zeros((mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
     pad[:local.shape[0]] = local
-    out = torch.empty((ws * mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    dist.all_gather_into_tensor(out, pad.contiguous())
-    parts = [out[r * mx:r * mx + counts[r]] for r in range(ws)]
-    return torch.cat(parts, 0), counts
+    if dst is None:
+        out = torch.empty((ws * mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+        work = dist.all_gather_into_tensor(out, pad, async_op=async_op)
+        nbytes = {"sent": (ws - 1) * mx * rb, "received": (ws - 1) * mx * rb}
+    else:
+        out = None
+        if rank == dst:
+            out = torch.empty((ws * mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+            work = dist.gather(pad, list(out.chunk(ws, 0)), dst=dst, async_op=async_op)
+            nbytes = {"sent": 0, "received": (ws - 1) * mx * rb}
+        else:
+            work = dist.gather(pad, None, dst=dst, async_op=async_op)
+            nbytes = {"sent": mx * rb, "received": 0}
+
+    def finish():
+        res = None
+        if out is not None:
+            res = torch.cat([out[r * mx:r * mx + counts[r]] for r in range(ws)], 0)
+        if _into is not None:
+            if res is not None:
+                _into[_key] = res
+        return res
+    if async_op:
+        if _into is not None:
+            _into._pending.append((work, finish))
+        return None, counts, nbytes
+    return finish(), counts, nbytes
 
 
 def gather_results(keys: torch.Tensor, forecast: torch.Tensor | None, metrics: torch.Tensor | None = None,
-                   status: torch.Tensor | None = None, counts=None) -> dict:
+                   status: torch.Tensor | None = None, counts=None, dst: int | None = None,
+                   async_op: bool = False) -> Gathered:
     """The engine's final exchange: every rank's
     [S_g, k] int64 series keys, [S_g, 3, T] fp32 forecast blocks (yhat,
     yhat_lower, yhat_upper), [S_g, M] fp64 validation metrics and [S_g]
-    int32 fit status, all-gathered to every rank.  One count exchange, then
-    one tensor all-gather per array."""
+    int32 fit status.  ``dst=None``: all-gathered to every rank (north_star's
+    RCCL all-gather); ``dst=r``: gathered to rank r only (the caller that
+    assembles the frame — Spark's driver collecting applyInPandas output):
+    rank r receives the same bytes, the other ranks send their block once and
+    receive nothing.  One count exchange, then one collective per array.
+    ``async_op=True`` leaves the collectives in flight on the backend's stream
+    (the caller's next kernels overlap them); ``wait()`` the result first."""
     if counts is None:
         counts = gather_counts(keys.shape[0], keys.device)
-    out = {"counts": counts}
-    out["keys"], _ = gather_blocks(keys, counts)
-    if forecast is not None:
-        out["forecast"], _ = gather_blocks(forecast, counts)
-    if metrics is not None:
-        out["metrics"], _ = gather_blocks(metrics, counts)
-    if status is not None:
-        out["status"], _ = gather_blocks(status, counts)
+    out = Gathered()
+    out["counts"] = counts
+    tot = {"sent": 0, "received": 0}
+    for name, t in (("keys", keys), ("forecast", forecast), ("metrics", metrics), ("status", status)):
+        if t is None:
+            continue
+        res, _, nb = gather_blocks(t, counts, dst=dst, async_op=async_op, _into=out, _key=name)
+        if not async_op and res is not None:
+            out[name] = res
+        tot["sent"] += nb["sent"]
+        tot["received"] += nb["received"]
+    out["bytes"] = tot
     return out
 
 
@@ -91,8 +157,8 @@ def gather_frames(frame, key_cols=("store", "item"), device=None):
     it = torch.from_numpy(np.ascontiguousarray(ints)).to(dev)
     vt = torch.from_numpy(np.ascontiguousarray(vals)).to(dev)
     counts = gather_counts(it.shape[0], dev)
-    gi, _ = gather_blocks(it, counts)
-    gv, _ = gather_blocks(vt, counts)
+    gi, _, _ = gather_blocks(it, counts)
+    gv, _, _ = gather_blocks(vt, counts)
     gi, gv = gi.cpu().numpy(), gv.cpu().numpy()
     out = {"ds": gi[:, 0].astype("datetime64[ns]")}
     for j, k in enumerate(key_cols):

@@ -141,7 +141,13 @@ typedef struct {
 int pf_ctx_create(int device, pf_ctx **out);
 int pf_ctx_destroy(pf_ctx *ctx);
 const char *pf_last_error(pf_ctx *ctx);
+/* Defaults every caller should start from (Stan optimizing() + the engine's
+ * polish settings); a zero-initialised pf_fit_opts is not a valid default. */
 void pf_default_fit_opts(pf_fit_opts *o);
+/* Build id: 32 hex digits of SHA-256 over the library's sources and compile
+ * flags (no reference counterpart; the Python loader refuses a library whose
+ * id does not match the sources it ships with).                            */
+const char *pf_build_id(void);
 
 /* Per-kernel timing (measurement only; no reference counterpart).  When
  * enabled, every launch is bracketed by HIP events on its own stream;

@@ -28,7 +28,7 @@ def _worker(rank, world, port, q):
         # stand-in for the per-rank forecast block: [n_r, 3] = (store, item, f(store, item))
         k = keys[mine]
         local = torch.from_numpy(np.column_stack([k, k[:, 0] * 1000 + k[:, 1]]).astype(np.float32))
-        allb, counts = parallel.gather_blocks(local)
+        allb, counts, _ = parallel.gather_blocks(local)
         q.put((rank, mine.tolist(), allb.numpy().tolist(), counts))
     finally:
         dist.destroy_process_group()
@@ -94,8 +94,22 @@ def _worker_results(rank, world, port, q):
         g = parallel.gather_results(torch.from_numpy(keys[mine].astype(np.int64)), torch.from_numpy(fc),
                                     torch.from_numpy(met), torch.from_numpy(st))
         fr = parallel.gather_frames(_frame(keys[mine], fc))
+        # gather to rank 0 only, and the asynchronous form of both
+        g0 = parallel.gather_results(torch.from_numpy(keys[mine].astype(np.int64)), torch.from_numpy(fc),
+                                     torch.from_numpy(met), torch.from_numpy(st), dst=0)
+        ga = parallel.gather_results(torch.from_numpy(keys[mine].astype(np.int64)), torch.from_numpy(fc),
+                                     torch.from_numpy(met), torch.from_numpy(st), async_op=True).wait()
+        ga0 = parallel.gather_results(torch.from_numpy(keys[mine].astype(np.int64)), torch.from_numpy(fc),
+                                      torch.from_numpy(met), torch.from_numpy(st), dst=0,
+                                      async_op=True).wait()
+        extra = dict(bytes=g["bytes"], bytes0=g0["bytes"], has0=sorted(k for k in g0 if k not in ("counts", "bytes")))
+        if rank == 0:
+            for name in ("keys", "forecast", "metrics", "status"):
+                assert torch.equal(g0[name], g[name]) and torch.equal(ga0[name], g[name]), name
+        for name in ("keys", "forecast", "metrics", "status"):
+            assert torch.equal(ga[name], g[name]), name
         q.put((rank, g["counts"], g["keys"].numpy(), g["forecast"].numpy(), g["metrics"].numpy(),
-               g["status"].numpy(), fr))
+               g["status"].numpy(), fr, extra))
     finally:
         dist.destroy_process_group()
 
@@ -119,8 +133,16 @@ def test_gloo_world2_gathers_real_shapes_equal_world1():
     fc1, met1, st1 = _series_outputs(keys)          # world-1 output
     ref = {tuple(k): i for i, k in enumerate(keys.tolist())}
     fr1 = _frame(keys, fc1).sort_values(["store", "item", "ds"]).reset_index(drop=True)
-    for rank, counts, gk, gf, gm, gs, fr in res:
+    row = 8 * 2 + 4 * 3 * TF + 8 * 4 + 4          # keys, forecast, metrics, status bytes per series
+    for rank, counts, gk, gf, gm, gs, fr, extra in res:
         assert sum(counts) == 500 and len(counts) == 2
+        mx = max(counts)
+        assert extra["bytes"] == {"sent": mx * row, "received": mx * row}
+        if rank == 0:
+            assert extra["bytes0"] == {"sent": 0, "received": mx * row}
+            assert extra["has0"] == ["forecast", "keys", "metrics", "status"]
+        else:
+            assert extra["bytes0"] == {"sent": mx * row, "received": 0} and extra["has0"] == []
         assert gf.shape == (500, 3, TF) and gf.dtype == np.float32
         assert gm.shape == (500, 4) and gm.dtype == np.float64 and gs.dtype == np.int32
         idx = np.array([ref[tuple(k)] for k in gk.tolist()])

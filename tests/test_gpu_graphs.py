@@ -113,3 +113,35 @@ def test_replay_after_a_larger_fit_on_the_same_engine():
         assert _bits_equal(e[k], r[k]), k
     for k in ("yhat", "yhat_lower", "yhat_upper"):
         assert torch.equal(e[k][:, :st.Tf], r[k][:, :st.Tf]), k
+
+
+def test_close_releases_the_private_context():
+    """a step that made its own engine destroys that pf_ctx on
+    close(); the shared per-device context and a caller-given private engine
+    are left alone; a closed step cannot replay."""
+    ds = synthetic.daily_dates("2016-01-01", "2017-12-31")
+    n = 8
+    Y = synthetic.sales_matrix(n, ds)
+    eng = dfa.Engine(0)
+    with dfa.ForecastStep(eng, ds, n) as st:
+        st.set_inputs(Y)
+        st.run()
+        st.capture()
+        st.replay()
+        ctx = st.engine.ctx
+        assert not ctx.closed
+    assert ctx.closed and st.graph is None
+    assert not eng.ctx.closed
+    with pytest.raises(RuntimeError, match="capture"):
+        st.replay()
+    own = dfa.Engine(0, own_context=True)
+    st2 = dfa.ForecastStep(own, ds, n)
+    assert st2.engine is own
+    st2.set_inputs(Y)
+    st2.run()
+    st2.close()
+    assert not own.ctx.closed
+    own.close()
+    assert own.ctx.closed
+    with pytest.raises(RuntimeError, match="shared"):
+        eng.ctx.close()

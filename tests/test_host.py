@@ -41,6 +41,38 @@ def test_missing_library_fails_loudly():
     assert "UNAVAILABLE" in out.stdout
 
 
+def test_build_id_matches_sources():
+    """The in-tree library was compiled from the committed csrc/ + include/."""
+    from distributed_forecasting_amd import build as bld
+    bid = _lib.check_build_id()
+    assert re.fullmatch(r"[0-9a-f]{32}", bid)
+    assert _lib.load().pf_build_id().decode() == bid == bld.source_hash()
+
+
+def test_stale_library_is_refused(tmp_path):
+    """A .so whose sources changed after it was built is refused (not loaded)."""
+    import shutil
+    from distributed_forecasting_amd import build as bld
+    csrc, inc = tmp_path / "csrc", tmp_path / "include"
+    shutil.copytree(bld.CSRC, csrc)
+    shutil.copytree(bld.INCLUDE, inc)
+    so = tmp_path / "libprophet_hip.so"
+    shutil.copy(bld.OUT, so)
+    assert _lib.check_build_id(str(so), str(csrc), str(inc)) == bld.source_hash()
+    with open(csrc / "pf_common.h", "a") as f:
+        f.write("\n// edited after the build\n")
+    with pytest.raises(_lib.EngineUnavailable, match="stale"):
+        _lib.check_build_id(str(so), str(csrc), str(inc))
+    # the same check guards load() of the in-tree path, in a fresh process
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from distributed_forecasting_amd import _lib, build\n"
+            "build.CSRC = %r\n"
+            "try:\n    _lib.load()\n"
+            "except _lib.EngineUnavailable as e:\n    print('REFUSED', e)\n") % (ROOT, str(csrc))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert "REFUSED" in out.stdout and "stale" in out.stdout, out.stdout + out.stderr
+
+
 def test_no_cpu_fallback_without_gpu():
     import torch
     if torch.cuda.is_available():
