@@ -66,16 +66,40 @@ def needs_build() -> bool:
     return embedded_id(OUT) != source_hash()
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
+# pf_engine.hip compiles as N_TU translation units (PF_TU = 0: host API and
+# non-fit kernels; 1..7: groups of fit-kernel instantiations) in parallel,
+# then links into one shared library
+N_TU = 8
+OBJ_DIR = os.path.join(_ROOT, "build", "pf_objs")
+
+
+def build(force: bool = False, verbose: bool = True, jobs: int | None = None) -> str:
     if not force and not needs_build():
         return OUT
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     bid = source_hash()
-    cmd = [hipcc, *FLAGS, f'-DPF_BUILD_ID="{bid}"',
-           "-I", INCLUDE, "-I", CSRC, "-o", OUT + ".tmp", *SOURCES]
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    jobs = jobs or min(N_TU, max(1, os.cpu_count() or 1), 16)
+    compile_flags = [f for f in FLAGS if f != "-shared"]
+    cmds = [[hipcc, *compile_flags, "-c", f"-DPF_TU={k}", f'-DPF_BUILD_ID="{bid}"',
+             "-I", INCLUDE, "-I", CSRC, "-o", os.path.join(OBJ_DIR, f"pf_tu{k}.o"), *SOURCES]
+            for k in range(N_TU)]
+    pending, running = list(cmds), []
+    while pending or running:
+        while pending and len(running) < jobs:
+            c = pending.pop(0)
+            if verbose:
+                print(" ".join(c), file=sys.stderr)
+            running.append((c, subprocess.Popen(c)))
+        c, pr = running.pop(0)
+        if pr.wait() != 0:
+            for _, q in running:
+                q.wait()
+            raise subprocess.CalledProcessError(pr.returncode, c)
+    link = [hipcc, *FLAGS, "-o", OUT + ".tmp"] + [os.path.join(OBJ_DIR, f"pf_tu{k}.o") for k in range(N_TU)]
     if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.check_call(cmd)
+        print(" ".join(link), file=sys.stderr)
+    subprocess.check_call(link)
     os.replace(OUT + ".tmp", OUT)
     return OUT
 

@@ -20,7 +20,21 @@
 
 #include "pf_common.h"
 #include "prophet_hip.h"
+
+// Split compilation (build.py): PF_TU = 0 compiles the host API and every
+// kernel outside the fit family; PF_TU = k >= 1 compiles the fit-kernel
+// instantiations of group k (launch_fitlike, listed at the end of the file),
+// so the groups build in parallel.  PF_TU undefined: one translation unit
+// with everything (diagnostic builds).
+#ifdef PF_TU
+#define PF_MAIN (PF_TU == 0)
+#else
+#define PF_MAIN 1
+#endif
+
+#if PF_MAIN
 #include "pf_cv.h"
+#endif
 #include "pf_ostat.h"
 
 #ifndef M_PI
@@ -122,6 +136,7 @@ static void timed_end(pf_ctx *ctx, int i, hipStream_t st) {
     timed_end(ctx, ti_, st);                                                     \
   } while (0)
 
+#if PF_MAIN
 // ============================================================================
 // K1: design builder
 // ============================================================================
@@ -486,6 +501,8 @@ __global__ __launch_bounds__(256) void k_prepare(int T, int Tp, const double *__
     status[s] = (vmin == vmax && growth != PF_GROWTH_LOGISTIC) ? PF_ST_CONSTANT : 0;
   }
 }
+
+#endif  // PF_MAIN (K1, prepare)
 
 // ============================================================================
 // K2/K3: objective + gradient (collective over one workgroup) and L-BFGS
@@ -2149,6 +2166,7 @@ __global__ __launch_bounds__(256) void k_predict_det(PredKArgs a0) {
 
 #include "pf_mc.h"
 
+#if PF_MAIN
 // ============================================================================
 // C ABI
 // ============================================================================
@@ -2462,8 +2480,11 @@ __global__ __launch_bounds__(256) void k_grid_rowmajor(const double *__restrict_
   XR[q] = f < K ? XT[(size_t)f * Tp + r] : 0.0;
 }
 
+#endif  // PF_MAIN (C ABI part 1, grid copies)
+
 // ---------------------------------------------------------------- dispatch
 #define PF_FIT_NW 4
+#if PF_MAIN
 namespace {
 
 FitKArgs make_fit_args(const pf_problem *pb) {
@@ -2496,6 +2517,9 @@ FitKArgs make_fit_args(const pf_problem *pb) {
   }
   return a;
 }
+
+}  // namespace
+#endif  // PF_MAIN
 
 enum { PF_LAUNCH_OBJGRAD = 0, PF_LAUNCH_FIT = 1, PF_LAUNCH_HESSIAN = 2 };
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
@@ -2611,6 +2635,37 @@ int launch_fitlike(pf_ctx *ctx, int what, const FitKArgs &a, int n, hipStream_t 
   return 0;
 }
 
+// The instantiations, grouped by translation unit (PF_TU = group): LG =
+// logistic, WD = wide (two parameter words).
+#define PF_LG PF_MODE_LOGI
+#define PF_WD PF_MODE_WIDE
+#define PF_FIT_INSTANCES(X)                                   \
+  X(1, 26, 10, 3, 0, MODE_MULT)                               \
+  X(2, 26, 10, 3, 0, MODE_ADD)                                \
+  X(2, 26, 10, 3, 0, MODE_MIXED)                              \
+  X(3, 36, 10, 3, 0, MODE_MULT | PF_LG)                       \
+  X(3, 36, 10, 3, 0, MODE_MULT)                               \
+  X(4, 44, 10, 3, 4, MODE_MULT | PF_LG | PF_WD)               \
+  X(4, 44, 10, 3, 4, MODE_MULT | PF_WD)                       \
+  X(5, 26, 10, 3, 0, MODE_MULT | PF_LG)                       \
+  X(5, 34, 10, 3, 4, MODE_MULT | PF_LG)                       \
+  X(6, 32, 0, 0, 0, MODE_MIXED | PF_LG)                       \
+  X(6, 32, 0, 0, 0, MODE_MIXED)                               \
+  X(7, 34, 10, 3, 4, MODE_MULT)                               \
+  X(7, 61, 0, 0, 0, MODE_MIXED)
+#define PF_FIT_NTU 8
+#ifdef PF_TU
+#if PF_TU == 0
+// the main unit uses the instances the fit units define
+#define PF_EXTERN_INST(G, K, O0, O1, O2, M)                                               \
+  extern template int launch_fitlike<PF_FIT_NW, K, O0, O1, O2, M>(pf_ctx *, int, const FitKArgs &, \
+                                                                  int, hipStream_t, double *);
+PF_FIT_INSTANCES(PF_EXTERN_INST)
+#endif
+#endif
+
+#if PF_MAIN
+namespace {
 // Template instances:
 //   (26, 10,3,0, MULT) — the reference's configuration (yearly 10 + weekly 3,
 //                        multiplicative): features regenerated in-register
@@ -2970,3 +3025,45 @@ int pf_cv_metrics(pf_ctx *ctx, const pf_cv_args *p, void *stream) {
 }
 
 }  // extern "C"
+#endif  // PF_MAIN (dispatch, C ABI part 2)
+
+// explicit instantiations of this fit unit's group (PF_EMIT_g expands to the
+// instantiation only in unit g)
+#if defined(PF_TU) && PF_TU >= 1
+#define PF_INST_BODY(K, O0, O1, O2, M)                                                     \
+  template int launch_fitlike<PF_FIT_NW, K, O0, O1, O2, M>(pf_ctx *, int, const FitKArgs &, int, \
+                                                           hipStream_t, double *);
+#define PF_SKIP(K, O0, O1, O2, M)
+#define PF_EMIT_1 PF_SKIP
+#define PF_EMIT_2 PF_SKIP
+#define PF_EMIT_3 PF_SKIP
+#define PF_EMIT_4 PF_SKIP
+#define PF_EMIT_5 PF_SKIP
+#define PF_EMIT_6 PF_SKIP
+#define PF_EMIT_7 PF_SKIP
+#if PF_TU == 1
+#undef PF_EMIT_1
+#define PF_EMIT_1 PF_INST_BODY
+#elif PF_TU == 2
+#undef PF_EMIT_2
+#define PF_EMIT_2 PF_INST_BODY
+#elif PF_TU == 3
+#undef PF_EMIT_3
+#define PF_EMIT_3 PF_INST_BODY
+#elif PF_TU == 4
+#undef PF_EMIT_4
+#define PF_EMIT_4 PF_INST_BODY
+#elif PF_TU == 5
+#undef PF_EMIT_5
+#define PF_EMIT_5 PF_INST_BODY
+#elif PF_TU == 6
+#undef PF_EMIT_6
+#define PF_EMIT_6 PF_INST_BODY
+#elif PF_TU == 7
+#undef PF_EMIT_7
+#define PF_EMIT_7 PF_INST_BODY
+#endif
+#define PF_DEF_INST(G, K, O0, O1, O2, M) PF_EMIT_##G(K, O0, O1, O2, M)
+PF_FIT_INSTANCES(PF_DEF_INST)
+#endif
+

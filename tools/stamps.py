@@ -4,7 +4,7 @@ import ctypes, os, subprocess, sys, time
 import numpy as np, torch
 sys.path.insert(0, ".")
 here = "distributed-forecasting_amd"
-out = os.path.join(here, "libprophet_hip_stamps.so")
+out = os.environ.get("PF_STAMPS_LIB") or os.path.abspath("diag_exp/libprophet_hip_stamps.so")
 if not os.path.exists(out):  # build here (CPU container), not on the GPU box
     subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
                        "-DPF_STAMPS", "-Iinclude", f"-I{here}/csrc", "-o", out, f"{here}/csrc/pf_engine.hip"])

@@ -4,7 +4,7 @@ import ctypes, os, sys
 import numpy as np, torch
 sys.path.insert(0, ".")
 from distributed_forecasting_amd import _lib
-_lib.load(os.path.abspath("distributed-forecasting_amd/libprophet_hip_stamps.so"))
+_lib.load(os.path.abspath("diag_exp/libprophet_hip_stamps.so"))
 import distributed_forecasting_amd as dfa
 from distributed_forecasting_amd import synthetic, batch as B
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 500

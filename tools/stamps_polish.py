@@ -8,7 +8,7 @@ import ctypes, os, sys
 import numpy as np, torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from distributed_forecasting_amd import _lib
-_lib.load(os.path.abspath(os.environ.get("PF_STAMPS_LIB", "distributed-forecasting_amd/libprophet_hip_stamps.so")))
+_lib.load(os.path.abspath(os.environ.get("PF_STAMPS_LIB", "diag_exp/libprophet_hip_stamps.so")))
 import distributed_forecasting_amd as dfa
 from distributed_forecasting_amd import synthetic, holidays as H
 from distributed_forecasting_amd.engine import ProphetConfig

@@ -5,7 +5,7 @@ import ctypes, os, subprocess, sys, time
 import numpy as np, torch
 sys.path.insert(0, ".")
 here = "distributed-forecasting_amd"
-out = os.environ.get("PF_STAMPS_LIB") or os.path.join(here, "libprophet_hip_stamps.so")
+out = os.environ.get("PF_STAMPS_LIB") or os.path.abspath("diag_exp/libprophet_hip_stamps.so")
 if not os.path.exists(out):
     subprocess.check_call(["sh", "tools/build_stamps.sh"])
 from distributed_forecasting_amd import _lib
