@@ -61,7 +61,8 @@ class PfFitOpts(ctypes.Structure):
                 ("tol_rel_grad", ctypes.c_double), ("tol_param", ctypes.c_double),
                 ("max_iter", i32), ("history", i32), ("polish", i32), ("polish_max_iter", i32),
                 ("lbfgs_warmup", i32), ("lbfgs_warmup_evals", i32), ("tile_min_series", i32),
-                ("polish_max_lag", i32), ("polish_lag_ratio", ctypes.c_double)]
+                ("polish_max_lag", i32), ("polish_lag_ratio", ctypes.c_double),
+                ("polish_lam0", ctypes.c_double)]
 
 
 class PfPredictArgs(ctypes.Structure):

@@ -68,23 +68,56 @@ __device__ __forceinline__ double cv_radix_select(const unsigned long long *keys
 }
 
 // One horizon group holding every row (in-sample metrics: rolling_mean_by_h
-// with w = n is the plain mean, rolling_median_by_h the median): the 64
-// lanes stride over the rows and reduce; the MDAPE median comes from two
-// radix selects (ranks (n-1)/2 and n/2) over the APE bit patterns.
-__device__ __forceinline__ void cv_single_group(const CvKArgs &a, int series, const double *y,
-                                                const float *yh, const float *lo, const float *hi,
-                                                unsigned long long *cache, int ncache, int *hist) {
-  const int lane = pf_lane(), n = a.n_rows;
+// with w = n is the plain mean, rolling_median_by_h the median): a block of
+// PF_CV_INS_WAVES waves per series strides over the rows (four independent
+// row loads in flight per thread), each wave reduces its sums, and wave 0 adds
+// the wave totals in a fixed order; the MDAPE median comes from two radix
+// selects (ranks (n-1)/2 and n/2) over the APE bit patterns cached in LDS.
+#define PF_CV_INS_WAVES 4
+#define PF_CV_INS_CACHE 3072
+__global__ __launch_bounds__(PF_CV_INS_WAVES * 64) void k_cv_insample(CvKArgs a) {
+  __shared__ unsigned long long s_cache[PF_CV_INS_CACHE];
+  __shared__ double s_part[PF_CV_INS_WAVES][6];
+  __shared__ int s_hist[256];
+  __shared__ int s_bad;
+  constexpr int NT = PF_CV_INS_WAVES * 64;
+  const int series = blockIdx.x, lane = pf_lane(), wave = pf_wave(), tid = threadIdx.x;
+  const double *y = a.y + (size_t)series * a.ld_y;
+  const float *yh = a.yhat + (size_t)series * a.ld_f;
+  const float *lo = a.ylo ? a.ylo + (size_t)series * a.ld_f : nullptr;
+  const float *hi = a.yhi ? a.yhi + (size_t)series * a.ld_f : nullptr;
+  const int n = a.n_rows;
+  const bool cached = n <= PF_CV_INS_CACHE;
+  if (tid == 0) s_bad = 0;
   double se = 0.0, ae = 0.0, ape = 0.0, sape = 0.0, cov = 0.0, ymin = INFINITY;
-  for (int r = lane; r < n; r += 64) {
-    const double yv = y[r], fv = (double)yh[r];
-    const double e = yv - fv;
-    se = fma(e, e, se);
-    ae += fabs(e);
-    ape += fabs(e / yv);
-    sape += 2.0 * fabs(e) / (fabs(yv) + fabs(fv));
-    if (lo) cov += (yv >= (double)lo[r] && yv <= (double)hi[r]) ? 1.0 : 0.0;
-    ymin = fmin(ymin, fabs(yv));
+  bool bad = false;
+  for (int r0 = tid; r0 < n; r0 += 4 * NT) {
+    double yv[4], fv[4];
+    bool in[4], ci[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int r = r0 + u * NT;
+      in[u] = r < n;
+      yv[u] = in[u] ? y[r] : 1.0;
+      fv[u] = in[u] ? (double)yh[r] : 1.0;
+      ci[u] = in[u] && lo && (yv[u] >= (double)lo[r] && yv[u] <= (double)hi[r]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (!in[u]) continue;
+      const double e = yv[u] - fv[u];
+      se = fma(e, e, se);
+      ae += fabs(e);
+      const double q = fabs(e / yv[u]);
+      ape += q;
+      sape += 2.0 * fabs(e) / (fabs(yv[u]) + fabs(fv[u]));
+      cov += ci[u] ? 1.0 : 0.0;
+      ymin = fmin(ymin, fabs(yv[u]));
+      if (!a.skip_mdape) {
+        bad |= (q != q);
+        if (cached) s_cache[r0 + u * NT] = (unsigned long long)__double_as_longlong(q);
+      }
+    }
   }
   se = wave_sum(se);
   ae = wave_sum(ae);
@@ -93,32 +126,41 @@ __device__ __forceinline__ void cv_single_group(const CvKArgs &a, int series, co
   cov = wave_sum(cov);
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) ymin = fmin(ymin, __shfl_xor(ymin, o, 64));
-  bool bad = false;
-  const bool cached = n <= ncache;
-  if (!a.skip_mdape) {
-    for (int r = lane; r < n; r += 64) {
-      const double v = fabs((y[r] - (double)yh[r]) / y[r]);
-      bad |= (v != v);
-      if (cached) cache[r] = (unsigned long long)__double_as_longlong(v);
-    }
+  if (lane == 0) {
+    s_part[wave][0] = se;
+    s_part[wave][1] = ae;
+    s_part[wave][2] = ape;
+    s_part[wave][3] = sape;
+    s_part[wave][4] = cov;
+    s_part[wave][5] = ymin;
   }
-  const bool anybad = __ballot(bad) != 0ull;
+  if (__ballot(bad) != 0ull && lane == 0) s_bad = 1;
+  __syncthreads();
+  if (wave != 0) return;   // no block-level sync below
+  double t[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  double tmin = INFINITY;
+#pragma unroll
+  for (int w = 0; w < PF_CV_INS_WAVES; ++w) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) t[k] += s_part[w][k];
+    tmin = fmin(tmin, s_part[w][5]);
+  }
+  const bool anybad = s_bad != 0;
   double v0 = NAN, v1 = NAN;
   if (!anybad && !a.skip_mdape) {
-    v0 = cv_radix_select(cached ? cache : nullptr, n, (n - 1) / 2, y, yh, hist);
-    v1 = (n % 2) ? v0 : cv_radix_select(cached ? cache : nullptr, n, n / 2, y, yh, hist);
+    v0 = cv_radix_select(cached ? s_cache : nullptr, n, (n - 1) / 2, y, yh, s_hist);
+    v1 = (n % 2) ? v0 : cv_radix_select(cached ? s_cache : nullptr, n, n / 2, y, yh, s_hist);
   }
   if (lane == 0) {
     double *m = a.metrics + (size_t)series * PF_CV_NMETRICS;
     const double w = (double)n;
-    const bool full = a.window <= n;   // a window larger than the rows yields nothing
-    m[PF_CV_MSE] = full ? se / w : NAN;
-    m[PF_CV_RMSE] = full ? sqrt(se / w) : NAN;
-    m[PF_CV_MAE] = full ? ae / w : NAN;
-    m[PF_CV_MAPE] = (full && ymin >= 1e-8) ? ape / w : NAN;
-    m[PF_CV_SMAPE] = full ? sape / w : NAN;
-    m[PF_CV_COVERAGE] = (full && lo) ? cov / w : NAN;
-    m[PF_CV_MDAPE] = (a.window <= n && !anybad && !a.skip_mdape) ? (v0 + v1) * 0.5 : NAN;
+    m[PF_CV_MSE] = t[0] / w;
+    m[PF_CV_RMSE] = sqrt(t[0] / w);
+    m[PF_CV_MAE] = t[1] / w;
+    m[PF_CV_MAPE] = (tmin >= 1e-8) ? t[2] / w : NAN;
+    m[PF_CV_SMAPE] = t[3] / w;
+    m[PF_CV_COVERAGE] = lo ? t[4] / w : NAN;
+    m[PF_CV_MDAPE] = (!anybad && !a.skip_mdape) ? (v0 + v1) * 0.5 : NAN;
   }
 }
 
@@ -130,11 +172,6 @@ __global__ __launch_bounds__(64) void k_cv_metrics(CvKArgs a) {
   const float *yh = a.yhat + (size_t)series * a.ld_f;
   const float *lo = a.ylo ? a.ylo + (size_t)series * a.ld_f : nullptr;
   const float *hi = a.yhi ? a.yhi + (size_t)series * a.ld_f : nullptr;
-  if (a.n_groups == 1 && a.window == a.n_rows) {
-    cv_single_group(a, series, y, yh, lo, hi, reinterpret_cast<unsigned long long *>(&s_sum[0][0]),
-                    PF_CV_MDAPE * PF_CV_GMAX, s_cnt);
-    return;
-  }
   double ymin = INFINITY;
   for (int g = lane; g < a.n_groups; g += 64) {
     double se = 0.0, ae = 0.0, ape = 0.0, sape = 0.0, cov = 0.0;

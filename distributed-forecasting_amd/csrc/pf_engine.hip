@@ -2278,6 +2278,7 @@ void pf_default_fit_opts(pf_fit_opts *o) {
   o->tile_min_series = 2048;
   o->polish_max_lag = 4;
   o->polish_lag_ratio = 1e-2;
+  o->polish_lam0 = 1e-4;    // damped first polish step (tools/diag_basin_floor.py)
 }
 
 int pf_num_changepoints(int T, int n_changepoints, double changepoint_range) {
@@ -2964,6 +2965,18 @@ int pf_predict(pf_ctx *ctx, const pf_predict_args *p, void *stream) {
       const int want = (8192 + a.n_series - 1) / a.n_series;  // blocks per series for ~8k blocks
       if (gx > want) gx = want;
       if (gx < 1) gx = 1;
+    } else {
+      // exact mode samples only the random rows (the horizon): a small batch
+      // spreads each series' rows over up to 8 blocks (each repeats the
+      // per-sample changepoint setup) so the kernel is not set by one block
+      // walking every horizon row
+      gx = (2048 + a.n_series - 1) / a.n_series;
+      if (gx > 8) gx = 8;
+      if (gx < 1) gx = 1;
+    }
+    if (const char *e = getenv("PF_MC_GX")) {   // diagnostic override
+      const int v = atoi(e);
+      if (v >= 1 && v <= 64) gx = v;
     }
     const dim3 gmc(gx, a.n_series);
     if (a.tr)
@@ -3018,8 +3031,12 @@ int pf_cv_metrics(pf_ctx *ctx, const pf_cv_args *p, void *stream) {
   a.ylo = p->yhat_lower;
   a.yhi = p->yhat_upper;
   a.metrics = p->metrics;
-  PF_TIMED_LAUNCH(ctx, "k_cv_metrics", p->n_series, (hipStream_t)stream, k_cv_metrics,
-                  dim3(p->n_series), dim3(64), 0, (hipStream_t)stream, a);
+  if (p->n_groups == 1 && p->window == p->n_rows)   // one group of every row: in-sample
+    PF_TIMED_LAUNCH(ctx, "k_cv_metrics", p->n_series, (hipStream_t)stream, k_cv_insample,
+                    dim3(p->n_series), dim3(PF_CV_INS_WAVES * 64), 0, (hipStream_t)stream, a);
+  else
+    PF_TIMED_LAUNCH(ctx, "k_cv_metrics", p->n_series, (hipStream_t)stream, k_cv_metrics,
+                    dim3(p->n_series), dim3(64), 0, (hipStream_t)stream, a);
   PF_HIP(ctx, hipGetLastError());
   return 0;
 }

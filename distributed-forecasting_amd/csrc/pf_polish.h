@@ -723,7 +723,11 @@ __device__ __forceinline__ bool polish_run(const FitKArgs &a, FitSmem<NW, KMAX, 
   bool cert = false;
   bool need_h = true;
   int lag = 0, ndamp = 0;
-  double lam = 0.0;
+  // the first QP's model is damped (pf_fit_opts.polish_lam0): an undamped
+  // first Newton step from the warm-up hand-off can jump into a neighbouring,
+  // worse local optimum (tools/diag_basin_floor.py / diag_basin_commit.py)
+  const double lam0 = a.o.polish_lam0 > 0.0 ? a.o.polish_lam0 : 0.0;
+  double lam = lam0;
   double dec_prev = 0.0;
   bool zero = false;    // QP active set (wave 0, lane = parameter)
   double sgn_ = 0.0;
@@ -811,7 +815,10 @@ __device__ __forceinline__ bool polish_run(const FitKArgs &a, FitSmem<NW, KMAX, 
     x = xn;
     f = fn;
     g = gn;
-    lam = (lam < 1e-9) ? 0.0 : lam * 0.1;
+    // the first step's damping ends with it; damping a non-positive pivot
+    // raised relaxes /10 per accepted step (oracle orc_polish_cfg2)
+    if (n_newton == 1 && lam <= lam0) lam = 0.0;
+    else lam = (lam < 1e-9) ? 0.0 : lam * 0.1;
     need_h = !(alpha == 1.0 && lag < a.o.polish_max_lag && lam == 0.0);
     lag = need_h ? 0 : lag + 1;
     dec_prev = dec;

@@ -132,6 +132,12 @@ typedef struct {
    * 1e-2.                                                                  */
   int32_t polish_max_lag;
   double polish_lag_ratio;
+  /* engine polish: the first QP's model is H + polish_lam0 * max|diag H| * I
+   * (one Levenberg-Marquardt-damped step; later steps undamped unless a
+   * non-positive pivot asks for damping).  An undamped first Newton step from
+   * the warm-up hand-off can jump to a neighbouring, worse local optimum of
+   * the non-convex MAP objective.  Default 1e-4; 0 = undamped.             */
+  double polish_lam0;
 } pf_fit_opts;
 
 /* component blocks pf_predict can report (seasonalities, holidays, ...) */

@@ -807,8 +807,9 @@ int orc_qp_active(const double *H, const double *gh, const double *x, int P, int
  * predicts zero decrease exactly at a KKT point, so the certificate
  * (dec >= -1e-15 |f| after a QP solved to KKT) is unchanged.  cert_out = 1
  * when the loop ended on that certificate. */
-int orc_polish_ex(const orc_problem *pb, double *theta, int max_it, int damp, double *f_out,
-                  int *n_newton, int *n_eval, int *n_solve, int *cert_out) {
+int orc_polish_cfg2(const orc_problem *pb, double *theta, int max_it, int damp, double lam0,
+                    double lam_decay, double alpha_first,
+                    double *f_out, int *n_newton, int *n_eval, int *n_solve, int *cert_out) {
     const int S = pb->S, P = 3 + S + pb->K;
     const double c = 1.0 / pb->tau;
     if (P > PMAX) return -1;
@@ -817,7 +818,7 @@ int orc_polish_ex(const orc_problem *pb, double *theta, int max_it, int damp, do
     evaluator ev = {pb, 0};
     if (feval(&ev, theta, &f, g)) return -2;
     int it, ns = 0, cert = 0, nn = 0;
-    double lam = 0.0;
+    double lam = lam0;
     for (it = 0; it < max_it; ++it) {
         for (int p = 0; p < P; ++p) gh[p] = g[p];
         for (int j = 0; j < S; ++j) gh[2 + j] -= c * sgn(theta[2 + j]);
@@ -839,7 +840,7 @@ int orc_polish_ex(const orc_problem *pb, double *theta, int max_it, int damp, do
         for (int j = 0; j < S; ++j) { l1z += fabs(z[2 + j]); l1x += fabs(theta[2 + j]); }
         dec += c * (l1z - l1x);
         if (dec > -1e-15 * fabs(f)) { cert = 1; break; }
-        double alpha = 1.0;
+        double alpha = (nn == 0) ? alpha_first : 1.0;
         int ok = 0;
         for (int ls = 0; ls < 30; ++ls) {
             for (int p = 0; p < P; ++p) xn[p] = theta[p] + alpha * d[p];
@@ -851,7 +852,10 @@ int orc_polish_ex(const orc_problem *pb, double *theta, int max_it, int damp, do
         memcpy(theta, xn, P * sizeof(double));
         memcpy(g, gn, P * sizeof(double));
         f = fn;
-        lam = (lam < 1e-9) ? 0.0 : lam * 0.1;
+        /* the first step's damping (lam0) ends with it; damping raised by a
+         * non-positive pivot relaxes x lam_decay per accepted step */
+        if (nn == 1 && lam <= lam0) lam = 0.0;
+        else lam = (lam < 1e-9) ? 0.0 : lam * lam_decay;
     }
     *f_out = f;
     *n_newton = nn;
@@ -859,6 +863,25 @@ int orc_polish_ex(const orc_problem *pb, double *theta, int max_it, int damp, do
     *n_solve = ns;
     if (cert_out) *cert_out = cert;
     return 0;
+}
+
+int orc_polish_cfg(const orc_problem *pb, double *theta, int max_it, int damp, double lam0,
+                   double *f_out, int *n_newton, int *n_eval, int *n_solve, int *cert_out) {
+    return orc_polish_cfg2(pb, theta, max_it, damp, lam0, 0.1, 1.0, f_out, n_newton, n_eval, n_solve,
+                           cert_out);
+}
+
+/* The engine's default: the first QP's model is damped by ORC_POLISH_LAM0 *
+ * max|diag H| (pf_fit_opts.polish_lam0).  An undamped first Newton step from
+ * a warm-up iterate can jump into a neighbouring, worse local optimum of the
+ * non-convex MAP objective (tools/diag_basin_commit.py: the polish from Stan
+ * iteration 60 lands 3e-5 .. 5e-4 above the MAP that the polish from
+ * iterations 50 or 70 reaches); one damped step keeps it in the basin. */
+#define ORC_POLISH_LAM0 1e-4
+int orc_polish_ex(const orc_problem *pb, double *theta, int max_it, int damp, double *f_out,
+                  int *n_newton, int *n_eval, int *n_solve, int *cert_out) {
+    return orc_polish_cfg(pb, theta, max_it, damp, damp ? ORC_POLISH_LAM0 : 0.0, f_out, n_newton, n_eval,
+                          n_solve, cert_out);
 }
 
 int orc_polish(const orc_problem *pb, double *theta, int max_it, double *f_out,

@@ -174,18 +174,26 @@ def hessian_fd(pb: po.Problem, theta, h=1e-6):
     return H
 
 
-def polish(pb: po.Problem, theta, max_it=20, damp=False, return_cert=False):
+POLISH_LAM0 = 1e-4   # stan_lbfgs.c ORC_POLISH_LAM0 = pf_default_fit_opts().polish_lam0
+
+
+def polish(pb: po.Problem, theta, max_it=20, damp=False, return_cert=False, lam0=None,
+           lam_decay=0.1, alpha_first=1.0):
     """Exact-MAP proximal-Newton polish (engine extension; same algorithm as
     the HIP kernel).  ``damp``: Levenberg-Marquardt damping when the exact
-    Hessian model is not positive definite.  Returns (theta, f, n_newton,
+    Hessian model is not positive definite, and (``lam0``, default
+    POLISH_LAM0 with damping) a damped first step.  Returns (theta, f, n_newton,
     n_eval, n_solve[, certified])."""
+    if lam0 is None:          # the engine's default: damped first step (with damping on)
+        lam0 = POLISH_LAM0 if damp else 0.0
     pin = _Pinned(pb)
     th = np.array(theta, dtype=np.float64, copy=True)
     f = ctypes.c_double()
     nn, ne, ns, cert = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-    rc = lib().orc_polish_ex(ctypes.byref(pin.c), th.ctypes.data_as(ctypes.c_void_p), int(max_it),
-                             int(bool(damp)), ctypes.byref(f), ctypes.byref(nn), ctypes.byref(ne),
-                             ctypes.byref(ns), ctypes.byref(cert))
+    rc = lib().orc_polish_cfg2(ctypes.byref(pin.c), th.ctypes.data_as(ctypes.c_void_p), int(max_it),
+                               int(bool(damp)), ctypes.c_double(lam0), ctypes.c_double(lam_decay),
+                               ctypes.c_double(alpha_first), ctypes.byref(f), ctypes.byref(nn),
+                               ctypes.byref(ne), ctypes.byref(ns), ctypes.byref(cert))
     if rc:
         raise ValueError(f"orc_polish failed ({rc})")
     out = (th, f.value, nn.value, ne.value, ns.value)
