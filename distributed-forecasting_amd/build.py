@@ -73,16 +73,22 @@ N_TU = 8
 OBJ_DIR = os.path.join(_ROOT, "build", "pf_objs")
 
 
-def build(force: bool = False, verbose: bool = True, jobs: int | None = None) -> str:
-    if not force and not needs_build():
+def build(force: bool = False, verbose: bool = True, jobs: int | None = None,
+          out: str | None = None, defines=()) -> str:
+    """Compile the library (in-tree ``OUT`` by default).  ``out`` + ``defines``
+    build a diagnostic variant (e.g. -DPF_STAMPS) elsewhere; it is never the
+    library ``_lib.load()`` checks."""
+    if out is None and not force and not needs_build():
         return OUT
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     bid = source_hash()
-    os.makedirs(OBJ_DIR, exist_ok=True)
+    target = OUT if out is None else os.path.abspath(out)
+    obj_dir = OBJ_DIR if out is None else target + ".objs"
+    os.makedirs(obj_dir, exist_ok=True)
     jobs = jobs or min(N_TU, max(1, os.cpu_count() or 1), 16)
     compile_flags = [f for f in FLAGS if f != "-shared"]
-    cmds = [[hipcc, *compile_flags, "-c", f"-DPF_TU={k}", f'-DPF_BUILD_ID="{bid}"',
-             "-I", INCLUDE, "-I", CSRC, "-o", os.path.join(OBJ_DIR, f"pf_tu{k}.o"), *SOURCES]
+    cmds = [[hipcc, *compile_flags, "-c", f"-DPF_TU={k}", f'-DPF_BUILD_ID="{bid}"', *defines,
+             "-I", INCLUDE, "-I", CSRC, "-o", os.path.join(obj_dir, f"pf_tu{k}.o"), *SOURCES]
             for k in range(N_TU)]
     pending, running = list(cmds), []
     while pending or running:
@@ -96,13 +102,16 @@ def build(force: bool = False, verbose: bool = True, jobs: int | None = None) ->
             for _, q in running:
                 q.wait()
             raise subprocess.CalledProcessError(pr.returncode, c)
-    link = [hipcc, *FLAGS, "-o", OUT + ".tmp"] + [os.path.join(OBJ_DIR, f"pf_tu{k}.o") for k in range(N_TU)]
+    link = [hipcc, *FLAGS, "-o", target + ".tmp"] + [os.path.join(obj_dir, f"pf_tu{k}.o") for k in range(N_TU)]
     if verbose:
         print(" ".join(link), file=sys.stderr)
     subprocess.check_call(link)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(target + ".tmp", target)
+    return target
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    # python build.py [--force] [--out PATH] [-DNAME ...]
+    args = sys.argv[1:]
+    o = args[args.index("--out") + 1] if "--out" in args else None
+    build(force="--force" in args, out=o, defines=[a for a in args if a.startswith("-D")])

@@ -567,6 +567,7 @@ struct FitKArgs {
   pf_fit_opts o;
   int pass;      // 0: first L-BFGS pass; >0: resume series the polish did not certify
   int warm_cap;  // this pass's iteration cap is the warm-up cap (MAXIT -> WARMUP)
+  int hstash;    // polish LDS holds the undamped-Hessian stash (FitSmem::hst)
   // ragged batch (pf_problem.grids): series s fits on grids[grid_of[s]]; that
   // grid's lane-blocked copy sits at rg_base + g * rg_stride bytes (same
   // layout as tP / XTP / sgP with the grid's own R, TQ); NULL: one grid
@@ -735,6 +736,7 @@ struct FitSmem {
   LbLds<ModeTr<MODE>::PW> *lb; // U view (Stan phase)
   int LD;           // stride of the polish matrix A in U
   double *pmt, *prho;  // polish, logistic: [32][32] d m_s / d theta, [32] segment sums
+  double *hst;         // polish: packed upper triangle of the undamped Hessian (FitKArgs.hstash)
   static __host__ __device__ size_t fixed_doubles(int ny) {
     return (size_t)ny + 64 * 4 + 2 * KMAX + 2 * NL + 2 * NW + 128 + NW + 128 + 4 + 4 +
            (size_t)NW * NSET * KMAX + 256 + 32 + 32 + 4 + 4 * 64;
@@ -746,16 +748,23 @@ struct FitSmem {
     const size_t red = (size_t)NTILE * 4 * 64;
     return ((a > red ? a : red) + 1) & ~(size_t)1;
   }
-  static __host__ __device__ size_t union_bytes(int P, int S, bool polish) {
+  // logistic tables after the polish matrix, then (optional) the stash of the
+  // undamped Hessian's upper triangle (polish_run: the damped first step's
+  // Hessian serves the next, undamped QP without a recomputation)
+  static __host__ __device__ size_t logi_doubles() {
+    return ((MODE & PF_MODE_LOGI) != 0) ? (32 * 32 + 32) : 0;
+  }
+  static __host__ __device__ size_t stash_doubles(int P) { return (size_t)P * (P + 1) / 2; }
+  static __host__ __device__ size_t union_bytes(int P, int S, bool polish, bool stash = false) {
     (void)S;
     const size_t lbb = sizeof(LbLds<ModeTr<MODE>::PW>) + 16;
     if (!polish) return lbb;
-    const size_t extra = ((MODE & PF_MODE_LOGI) != 0) ? (32 * 32 + 32) : 0;
-    const size_t hm = (polish_head_doubles(P) + extra) * sizeof(double);
+    const size_t hm = (polish_head_doubles(P) + logi_doubles() + (stash ? stash_doubles(P) : 0)) *
+                      sizeof(double);
     return lbb > hm ? lbb : hm;
   }
-  static __host__ __device__ size_t bytes(int ny, int P, int S, bool polish) {
-    return fixed_doubles(ny) * sizeof(double) + union_bytes(P, S, polish) + 64;
+  static __host__ __device__ size_t bytes(int ny, int P, int S, bool polish, bool stash = false) {
+    return fixed_doubles(ny) * sizeof(double) + union_bytes(P, S, polish, stash) + 64;
   }
   __device__ void carve(char *base, int ny, int P) {
     double *p = reinterpret_cast<double *>(base);
@@ -793,6 +802,7 @@ struct FitSmem {
     LD = P | 1;
     pmt = U + polish_head_doubles(P);
     prho = pmt + 32 * 32;
+    hst = pmt + logi_doubles();
   }
 };
 
@@ -927,11 +937,21 @@ __device__ __forceinline__ void eval_rows(const FitKArgs &a, FitSmem<NW, KMAX, M
   double rr = 0.0, acc0 = 0.0, acc1 = 0.0;
   RowIn cur;
   if (R > 0) load_rowp<O0, O1, O2>(a, L, cur);
+#ifdef PF_ROW_PF2
+  // rows loaded two ahead (the grid copy is an L2 hit; one row of FP64 work
+  // does not cover its latency)
+  RowIn nx1;
+  if (R > 1) load_rowp<O0, O1, O2>(a, NL + L, nx1);
+#endif
   for (int r = 0; r < R; ++r) {
     const int q = r * NL + L;       // lane-blocked position
     const int i = L * R + r;        // natural row
     RowIn nxt;
+#ifdef PF_ROW_PF2
+    if (r + 2 < R) load_rowp<O0, O1, O2>(a, q + 2 * NL, nxt);
+#else
     if (r + 1 < R) load_rowp<O0, O1, O2>(a, q + NL, nxt);
+#endif
     const bool valid = i < T;
     const double ti = cur.t;
     const int sg = cur.seg;
@@ -984,7 +1004,12 @@ __device__ __forceinline__ void eval_rows(const FitKArgs &a, FitSmem<NW, KMAX, M
     }
     acc0 += A0;
     acc1 += A1;
+#ifdef PF_ROW_PF2
+    cur = nx1;
+    nx1 = nxt;
+#else
     cur = nxt;
+#endif
   }
   PF_STAMP(2);
   // thread totals -> inclusive suffix within the wave + wave totals
@@ -1257,23 +1282,39 @@ __global__ __launch_bounds__(NW * 64) void k_objgrad(FitKArgs a0) {
 // ---------------------------------------------------------------- L-BFGS (Stan 2.19 restatement)
 __device__ __forceinline__ double cubic_interp0(double df0, double x1, double f1, double df1,
                                                 double loX, double hiX) {
+#ifdef PF_FAST_CUBIC
+  // two reciprocals instead of nine divisions (Stan's CubicInterp values up
+  // to rounding)
+  const double ix = 1.0 / x1;
+  const double c3 = (-12 * f1 + 6 * x1 * (df0 + df1)) * (ix * ix * ix);
+  const double c2 = -(4 * df0 + 2 * df1) * ix + 6 * f1 * (ix * ix);
+  const double c1 = df0;
+  const double t_s = sqrt(c2 * c2 - 2.0 * c1 * c3);
+  const double ic3 = 1.0 / c3;
+  const double s1 = -(c2 + t_s) * ic3;
+  const double s2 = -(c2 - t_s) * ic3;
+  const double c33 = c3 * (1.0 / 3.0);
+  auto poly = [&](double x) { return x * (x * (x * c33 + c2) * 0.5 + c1); };
+#else
   const double c3 = (-12 * f1 + 6 * x1 * (df0 + df1)) / (x1 * x1 * x1);
   const double c2 = -(4 * df0 + 2 * df1) / x1 + 6 * f1 / (x1 * x1);
   const double c1 = df0;
   const double t_s = sqrt(c2 * c2 - 2.0 * c1 * c3);
   const double s1 = -(c2 + t_s) / c3;
   const double s2 = -(c2 - t_s) / c3;
+  auto poly = [&](double x) { return x * (x * (x * c3 / 3.0 + c2) / 2.0 + c1); };
+#endif
   double tmpF, minF, minX;
-  minF = loX * (loX * (loX * c3 / 3.0 + c2) / 2.0 + c1);
+  minF = poly(loX);
   minX = loX;
-  tmpF = hiX * (hiX * (hiX * c3 / 3.0 + c2) / 2.0 + c1);
+  tmpF = poly(hiX);
   if (tmpF < minF) { minF = tmpF; minX = hiX; }
   if (loX < s1 && s1 < hiX) {
-    tmpF = s1 * (s1 * (s1 * c3 / 3.0 + c2) / 2.0 + c1);
+    tmpF = poly(s1);
     if (tmpF < minF) { minF = tmpF; minX = s1; }
   }
   if (loX < s2 && s2 < hiX) {
-    tmpF = s2 * (s2 * (s2 * c3 / 3.0 + c2) / 2.0 + c1);
+    tmpF = poly(s2);
     if (tmpF < minF) { minF = tmpF; minX = s2; }
   }
   return minX;
@@ -1674,12 +1715,14 @@ __device__ __forceinline__ bool lbfgs_advance(const pf_fit_opts &o, LbLds<PW> &L
   int state = __builtin_amdgcn_readfirstlane(L.state);
   // every scalar of the optimizer is wave-uniform: say so (SGPRs + scalar
   // branches instead of exec-masked control flow)
+#ifndef PF_NO_RFL_Z
   {
     static_assert(sizeof(LbScalars) % 4 == 0, "LbScalars words");
     int *w = reinterpret_cast<int *>(&z);
 #pragma unroll
     for (int i = 0; i < (int)(sizeof(LbScalars) / 4); ++i) w[i] = __builtin_amdgcn_readfirstlane(w[i]);
   }
+#endif
   PV<PW> xk, gk, pk;
 #pragma unroll
   for (int h = 0; h < PW; ++h) {
@@ -1918,15 +1961,25 @@ __global__ __launch_bounds__(NW * 64, FitOcc<KMAX>::W) void k_polish_resume(FitK
 // The two phases are separate (non-inlined) functions so each gets its own
 // register allocation: inlined together, the polish's pressure spilled
 // values of the L-BFGS evaluation loop.
+#ifdef PF_FUSE_INLINE
+#define PF_PHASE_ATTR __forceinline__
+#else
+#define PF_PHASE_ATTR __noinline__
+#endif
+#ifdef PF_FUSE_INLINE_FIT
+#define PF_FIT_PHASE_ATTR __forceinline__
+#else
+#define PF_FIT_PHASE_ATTR PF_PHASE_ATTR
+#endif
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
-__device__ __noinline__ void fit_phase(const FitKArgs &a, int pass, int max_iter, bool warm) {
+__device__ PF_FIT_PHASE_ATTR void fit_phase(const FitKArgs &a, int pass, int max_iter, bool warm) {
   pf_fit_opts o = a.o;
   o.max_iter = max_iter;
   if (!warm) o.lbfgs_warmup_evals = 0;
   fit_body<NW, KMAX, O0, O1, O2, MODE>(a, pass, o, warm);
 }
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
-__device__ __noinline__ void polish_phase(const FitKArgs &a) {
+__device__ PF_PHASE_ATTR void polish_phase(const FitKArgs &a) {
   polish_body<NW, KMAX, O0, O1, O2, MODE>(a);
 }
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
@@ -2194,17 +2247,6 @@ int pf_ctx_create(int device, pf_ctx **out) {
   return 0;
 }
 
-#ifdef PF_STAMPS
-int pf_debug_stamps(unsigned long long *out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pf_dbg), sizeof(unsigned long long) * 32) != hipSuccess) return -2;
-  if (reset) {
-    unsigned long long z[32] = {0};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(pf_dbg), z, sizeof z) != hipSuccess) return -2;
-  }
-  return 0;
-}
-#endif
-
 int pf_set_timing(pf_ctx *ctx, int enable) {
   if (!ctx) return set_err(nullptr, "pf_set_timing: NULL ctx");
   ctx->timing = enable ? 1 : 0;
@@ -2272,7 +2314,7 @@ void pf_default_fit_opts(pf_fit_opts *o) {
   o->max_iter = 10000;
   o->history = 5;
   o->polish = 1;
-  o->polish_max_iter = 50;  // accepted Newton steps (damped logistic fits from far away need ~30)
+  o->polish_max_iter = 100;  // Newton steps (damped logistic fits from far away need up to ~52)
   o->lbfgs_warmup = 60;
   o->lbfgs_warmup_evals = 90;  // also end a warm-up pass at 90 evaluations (tools/diag_warmup.py)
   o->tile_min_series = 2048;
@@ -2524,11 +2566,32 @@ FitKArgs make_fit_args(const pf_problem *pb) {
 
 enum { PF_LAUNCH_OBJGRAD = 0, PF_LAUNCH_FIT = 1, PF_LAUNCH_HESSIAN = 2 };
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
+int launch_fitlike_impl(pf_ctx *ctx, int what, const FitKArgs &a, int n, hipStream_t st, double *H_out,
+                        size_t smem, size_t smem_p);
+template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
 int launch_fitlike(pf_ctx *ctx, int what, const FitKArgs &a, int n, hipStream_t st, double *H_out) {
   // the polish handles K <= 48 (three 16-column beta blocks) and 2 + S <= 32
   constexpr bool HAS_POLISH = KMAX <= 48;
   const size_t smem = FitSmem<NW, KMAX, MODE>::bytes(a.TQ, a.P, a.S, false);
-  const size_t smem_p = FitSmem<NW, KMAX, MODE>::bytes(a.TQ, a.P, a.S, HAS_POLISH);
+  size_t smem_p = FitSmem<NW, KMAX, MODE>::bytes(a.TQ, a.P, a.S, HAS_POLISH);
+  FitKArgs a2 = a;
+  a2.hstash = 0;
+  if (HAS_POLISH && a.o.polish_lam0 > 0.0) {
+    // the stash only where it keeps the workgroups per CU the kernel is built
+    // for (two at <= 80 KB each for the 2-waves/SIMD layouts)
+    const size_t with = FitSmem<NW, KMAX, MODE>::bytes(a.TQ, a.P, a.S, true, true);
+    const size_t cap = (FitOcc<KMAX>::W >= 2 && smem_p <= 80 * 1024) ? 80 * 1024 : 160 * 1024;
+    if (with <= cap) {
+      smem_p = with;
+      a2.hstash = 1;
+    }
+  }
+  return launch_fitlike_impl<NW, KMAX, O0, O1, O2, MODE>(ctx, what, a2, n, st, H_out, smem, smem_p);
+}
+template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
+int launch_fitlike_impl(pf_ctx *ctx, int what, const FitKArgs &a, int n, hipStream_t st, double *H_out,
+                        size_t smem, size_t smem_p) {
+  constexpr bool HAS_POLISH = KMAX <= 48;
   if (smem > 160 * 1024) return set_err(ctx, "fit: series too long for the LDS budget");
   if (what == PF_LAUNCH_HESSIAN) {
     if constexpr (HAS_POLISH) {
@@ -2965,15 +3028,11 @@ int pf_predict(pf_ctx *ctx, const pf_predict_args *p, void *stream) {
       const int want = (8192 + a.n_series - 1) / a.n_series;  // blocks per series for ~8k blocks
       if (gx > want) gx = want;
       if (gx < 1) gx = 1;
-    } else {
-      // exact mode samples only the random rows (the horizon): a small batch
-      // spreads each series' rows over up to 8 blocks (each repeats the
-      // per-sample changepoint setup) so the kernel is not set by one block
-      // walking every horizon row
-      gx = (2048 + a.n_series - 1) / a.n_series;
-      if (gx > 8) gx = 8;
-      if (gx < 1) gx = 1;
     }
+    // (exact mode: one block per series.  More blocks per series repeat the
+    // per-sample changepoint setup and were slower at every batch size
+    // measured: 500 series, 1/2/4/8 blocks -> 0.198 / 0.236 / 0.316 / 0.449 ms,
+    // tools/time_tail.py, profiles/r04a_tail.log)
     if (const char *e = getenv("PF_MC_GX")) {   // diagnostic override
       const int v = atoi(e);
       if (v >= 1 && v <= 64) gx = v;
@@ -3084,3 +3143,16 @@ int pf_cv_metrics(pf_ctx *ctx, const pf_cv_args *p, void *stream) {
 PF_FIT_INSTANCES(PF_DEF_INST)
 #endif
 
+// diagnostic stamps read-back: defined in the unit whose kernels write the
+// stamps (each split unit has its own device copy of pf_dbg) — the
+// reference-layout fit unit, or the single unit
+#if defined(PF_STAMPS) && (!defined(PF_TU) || PF_TU == 1)
+extern "C" int pf_debug_stamps(unsigned long long *out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pf_dbg), sizeof(unsigned long long) * 32) != hipSuccess) return -2;
+  if (reset) {
+    unsigned long long z[32] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(pf_dbg), z, sizeof z) != hipSuccess) return -2;
+  }
+  return 0;
+}
+#endif

@@ -74,7 +74,8 @@ __device__ __forceinline__ void mfma_tiles(pf_d4 (&acc)[NT], const double (&lt)[
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
 __device__ __forceinline__ void hessian_collective(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm,
                                                    const PV<ModeTr<MODE>::PW> &x,
-                                                   const PV<ModeTr<MODE>::PW> &gh, double lam) {
+                                                   const PV<ModeTr<MODE>::PW> &gh, double lam,
+                                                   bool stash = false) {
   constexpr int PW = ModeTr<MODE>::PW;
   constexpr int NBB = FitSmem<NW, KMAX, MODE>::NBB;
   constexpr int NB = 2 + NBB;
@@ -374,6 +375,16 @@ __device__ __forceinline__ void hessian_collective(const FitKArgs &a, FitSmem<NW
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    if (stash) {
+      // the undamped H (packed upper triangle, row i from i (2P - i + 1) / 2)
+      // for the QP after the damped first step (polish_run)
+      for (int e = lane; e < P * P; e += 64) {
+        const int i = e / P, j = e - i * P;
+        if (j >= i) sm.hst[i * (2 * P - i + 1) / 2 + (j - i)] = A[i * LD + j];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
     if (lam > 0.0) {
 #pragma unroll
       for (int hw = 0; hw < PW; ++hw) {
@@ -708,6 +719,30 @@ __device__ __forceinline__ bool qp_active(const FitKArgs &a, FitSmem<NW, KMAX, M
 // zero decrease exactly at a KKT point, so the certificate holds either way;
 // oracle/stan_lbfgs.c:orc_polish_ex recomputes every iteration and reaches
 // the same MAP.
+// A <- the stashed undamped Hessian (hessian_collective with stash), padding
+// rows zeroed as the assembly leaves them.  Wave 0; the caller synchronises.
+template <int NW, int KMAX, int MODE>
+__device__ __forceinline__ void restore_hessian(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm) {
+  if (pf_wave() != 0) return;
+  const int lane = pf_lane();
+  const int P = __builtin_amdgcn_readfirstlane(a.P);
+  const int LD = __builtin_amdgcn_readfirstlane(sm.LD);
+  double *A = sm.U;
+  for (int e = lane; e < (P + 8) * LD; e += 64) A[e] = 0.0;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  for (int e = lane; e < P * P; e += 64) {
+    const int i = e / P, j = e - i * P;
+    if (j >= i) {
+      const double v = sm.hst[i * (2 * P - i + 1) / 2 + (j - i)];
+      A[i * LD + j] = v;
+      A[j * LD + i] = v;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
 #define PF_POLISH_MAXDAMP 24
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
 __device__ __forceinline__ bool polish_run(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm,
@@ -731,14 +766,27 @@ __device__ __forceinline__ bool polish_run(const FitKArgs &a, FitSmem<NW, KMAX, 
   double dec_prev = 0.0;
   bool zero = false;    // QP active set (wave 0, lane = parameter)
   double sgn_ = 0.0;
+  // the damped first step's Hessian is stashed undamped (FitKArgs.hstash):
+  // the next QP sweeps it in again instead of recomputing H at the new point
+  // (a lagged Hessian one short step old; the certificate holds for any
+  // positive-definite model)
+  bool stashed = false, restore = false;
   for (int it = 0; it < a.o.polish_max_iter;) {
     PV<PW> gh = g;
     if (isd) gh[0] = g[0] - c * (double)((x[0] > 0.0) - (x[0] < 0.0));
     const bool fresh = need_h;
+    const bool restored = fresh && restore;
     if (fresh) {
       PF_STAMP(20);
-      PF_COUNT(15);
-      hessian_collective<NW, KMAX, O0, O1, O2, MODE>(a, sm, x, gh, lam);
+      if (restored) {
+        restore_hessian<NW, KMAX, MODE>(a, sm);
+        restore = false;
+      } else {
+        PF_COUNT(15);
+        const bool st = a.hstash && n_newton == 0 && lam > 0.0 && lam <= lam0;
+        hessian_collective<NW, KMAX, O0, O1, O2, MODE>(a, sm, x, gh, lam, st);
+        stashed = st;
+      }
       __syncthreads();
       PF_STAMP(21);
       sweep_in_free<NW, KMAX, MODE>(a, sm, gh, c);
@@ -773,9 +821,10 @@ __device__ __forceinline__ bool polish_run(const FitKArgs &a, FitSmem<NW, KMAX, 
     __syncthreads();
     if (!qp_ok) {
       // warm QP failed: recompute the Hessian at the same point; cold QP
-      // failed (non-positive pivot): damp the model and recompute
+      // failed (non-positive pivot): damp the model and recompute (a failed
+      // QP on the restored stash first recomputes the exact Hessian)
       if (fresh) PF_COUNT(28); else PF_COUNT(29);
-      if (fresh) {
+      if (fresh && !restored) {
         if (++ndamp > PF_POLISH_MAXDAMP) break;
         lam = (lam == 0.0) ? 1e-10 : lam * 10.0;
       }
@@ -817,10 +866,21 @@ __device__ __forceinline__ bool polish_run(const FitKArgs &a, FitSmem<NW, KMAX, 
     g = gn;
     // the first step's damping ends with it; damping a non-positive pivot
     // raised relaxes /10 per accepted step (oracle orc_polish_cfg2)
-    if (n_newton == 1 && lam <= lam0) lam = 0.0;
-    else lam = (lam < 1e-9) ? 0.0 : lam * 0.1;
-    need_h = !(alpha == 1.0 && lag < a.o.polish_max_lag && lam == 0.0);
-    lag = need_h ? 0 : lag + 1;
+    if (n_newton == 1 && lam <= lam0) {
+      lam = 0.0;
+      restore = stashed;
+    } else {
+      lam = (lam < 1e-9) ? 0.0 : lam * 0.1;
+    }
+    stashed = false;
+    if (restore) {
+      need_h = true;   // the restored stash (a lagged Hessian: lag 1 after it)
+      lag = 0;
+    } else {
+      need_h = !(alpha == 1.0 && lag < a.o.polish_max_lag && lam == 0.0);
+      lag = need_h ? 0 : lag + 1;
+    }
+    if (restored) lag = need_h ? 0 : lag + 1;
     dec_prev = dec;
   }
   return cert;

@@ -200,7 +200,7 @@ def polish(pb: po.Problem, theta, max_it=20, damp=False, return_cert=False, lam0
     return out + (bool(cert.value),) if return_cert else out
 
 
-def fit_map(setup: po.FitSetup, opts=None, polish_it=50, damp=True):
+def fit_map(setup: po.FitSetup, opts=None, polish_it=100, damp=True):
     """Engine semantics on the CPU: Stan L-BFGS, then the exact-MAP polish
     (every growth mode; Levenberg-Marquardt damping where the Hessian model
     is not positive definite, as the kernel does)."""

@@ -123,14 +123,21 @@ def test_logistic_tile_matches_per_series(hourly):
     f_t, f_s = ft.f.cpu().numpy(), fs.f.cpu().numpy()
     if not hourly:
         assert np.all(st_t == 70) and np.all(st_s == 70), (st_t, st_s)
-    else:
-        # 60 days of hourly logistic data: an ill-conditioned fit, where the
-        # per-series path too leaves 3 of 21 series uncertified (Stan's
-        # endpoint, status 31); the tiled path certifies all but at most one more
-        assert (st_t == 70).sum() >= (st_s == 70).sum() - 1, (st_t, st_s)
+    # every series either path leaves uncertified (60 days of hourly logistic
+    # data is an ill-conditioned fit) still meets north_star's bar: objective
+    # no worse than the oracle's Stan endpoint + 1e-6 relative
+    cfg = dict(po.DEFAULT_CONFIG, growth="logistic")
+    cfg["daily"] = (1.0, 4) if hourly else None
+    for s in np.flatnonzero((st_t != 70) | (st_s != 70)):
+        setup = po.build_problem(ds, Y[s], cfg, cap=cap[s])
+        fo = so.fit_setup(setup)[1]
+        for name, f in (("tile", f_t[s]), ("series", f_s[s])):
+            assert f <= fo + 1e-6 * abs(fo), (name, s, f, fo, st_t[s], st_s[s])
     both = (st_t == 70) & (st_s == 70)
     assert both.sum() >= 17
     assert np.all(np.abs(f_t - f_s)[both] <= 1e-9 * np.abs(f_s)[both]), np.max(np.abs(f_t - f_s) / np.abs(f_s))
+    # the tiled pass certifies at least as many series as the per-series one
+    assert (st_t == 70).sum() >= (st_s == 70).sum() - 1, (st_t, st_s)
 
 
 @pytest.mark.parametrize("growth", ["linear", "logistic"])

@@ -1,5 +1,7 @@
 #!/bin/sh
-# Diagnostic library for tools/stamps.py (-DPF_STAMPS); never loaded by the product.
-cd "$(dirname "$0")/.." && exec /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared \
-  -DPF_STAMPS -Iinclude -Idistributed-forecasting_amd/csrc \
-  -o diag_exp/libprophet_hip_stamps.so distributed-forecasting_amd/csrc/pf_engine.hip
+# Diagnostic library for tools/stamps*.py (-DPF_STAMPS); never loaded by the product.
+# Extra -D flags are passed through (experiment variants): build_stamps.sh [OUT [-DX ...]]
+cd "$(dirname "$0")/.." || exit 1
+out="${1:-diag_exp/libprophet_hip_stamps.so}"
+[ $# -gt 0 ] && shift
+exec python distributed-forecasting_amd/build.py --out "$out" -DPF_STAMPS "$@"
