@@ -82,15 +82,13 @@ def test_tile_flat_growth_and_short_grid():
 
 
 def test_tile_default_size_matches_per_series():
-    """at the size where K3T runs by default (n = 4096 >=
-    tile_min_series = 2048, configs[2]'s generator, the persistent schedule
-    with slot refills): the default fit (warm-up hand-off to the polish)
-    certifies the same MAP as Stan's full run + polish (fit_mode stan_map)
-    on all but a measured <= 0.1 % of series — the warm-up hand-off can
-    certify a neighbouring local optimum (1 of 4096 here, 4.6e-4 relative;
-    tools/diag_tile_basin.py) — for the tiled and the per-series
-    first pass alike; where both reach stan_map's MAP their forecasts agree
-    within 1e-6 y_scale; refits are bitwise reproducible."""
+    """at the size where K3T runs by default
+    (n = 4096 >= tile_min_series = 2048, configs[2]'s generator, the
+    persistent schedule with slot refills) the default fit (warm-up hand-off
+    to the polish, whose first step is LM-damped) certifies the same MAP as
+    Stan's full run + polish (fit_mode stan_map) for the tiled and the
+    per-series first pass; their forecasts agree within 1e-6 y_scale;
+    refits are bitwise reproducible."""
     n = 4096
     e, g, ds, Y, Yd = _setup(n)
     ft = e.fit(g, Yd)                       # default: tiled first pass
@@ -98,16 +96,13 @@ def test_tile_default_size_matches_per_series():
     fs = e.fit(g, Yd, tile_min_series=-1)   # per-series kernel
     fm = e.fit(g, Yd, stan_faithful=True, tile_min_series=-1)
     f_m = fm.f.cpu().numpy()
-    ok = {}
     for name, fit in (("tile", ft), ("series", fs)):
         st = fit.status.cpu().numpy()
-        assert np.mean(st == 70) >= 0.999, (name, np.unique(st, return_counts=True))
+        assert np.all(st == 70), (name, np.unique(st, return_counts=True))
         rel = (fit.f.cpu().numpy() - f_m) / np.abs(f_m)
-        assert np.mean(rel > 1e-9) <= 1e-3, (name, int(np.sum(rel > 1e-9)))
-        assert rel.max() < 1e-3, (name, float(rel.max()))
-        ok[name] = (np.abs(rel) <= 1e-9) & (st == 70)
+        assert np.all(rel <= 1e-6), (name, int(np.sum(rel > 1e-6)), float(rel.max()))
+        assert np.all(np.abs(rel) <= 1e-9), (name, float(np.abs(rel).max()))
     assert torch.equal(ft.theta, ft2.theta) and torch.equal(ft.f, ft2.f)
-    both = ok["tile"] & ok["series"]
     fut = np.concatenate([ds, ds[-1] + synthetic.NS_PER_DAY * np.arange(1, 91)])
     fg = e.predict_grid(ft, fut)
     sid = torch.arange(n, dtype=torch.int32, device="cuda")
@@ -115,4 +110,30 @@ def test_tile_default_size_matches_per_series():
     os_ = e.predict(fs, fg, seed=0, components=False, series_id=sid)
     ys = ft.y_scale.cpu().numpy()[:, None]
     d = np.abs(ot["yhat"][:, :fg.T].double().cpu().numpy() - os_["yhat"][:, :fg.T].double().cpu().numpy()) / ys
-    assert np.all(d[both] <= 1e-6), float(d[both].max())
+    assert np.all(d <= 1e-6), float(d.max())
+
+
+@pytest.mark.parametrize("gen", [dict(config_index=1), dict(config_index=2), dict(seed=1001),
+                                 dict(seed=1002)])
+def test_default_fit_never_worse_than_stan_map(gen):
+    """North_star's objective bar, per series, at scale: 4 generator seeds x
+    4096 series (1826 days).  The default fit (60-iteration Stan warm-up ->
+    polish with an LM-damped first step) is never worse than Stan's full
+    L-BFGS run + polish (fit_mode stan_map) by more than 1e-6 relative — 0
+    series.  Before the damped first step 8 of these 16384 series certified
+    a neighbouring local optimum 3e-5 .. 5e-4 worse (profiles/
+    r04a_basin_floor_undamped.json; tools/diag_basin_commit.py shows the
+    undamped Newton step from Stan's iteration-60 point jumping basins while
+    the polish from iterations 50 or 70 does not)."""
+    e = dfa.Engine(0, ProphetConfig.reference())
+    ds = synthetic.daily_dates()
+    seasons = e.config.seasons(int(ds[0]), int(ds[-1]), int(ds[1] - ds[0]))
+    g = dfa.build_grid(ds, seasons, start_ns=int(ds[0]), t_scale_ns=int(ds[-1] - ds[0]))
+    n = 4096
+    Y = synthetic.sales_matrix(n, ds, **gen)
+    Yd = torch.zeros((n, g.T_pad), dtype=torch.float64, device="cuda")
+    Yd[:, :g.T] = torch.from_numpy(Y).cuda()
+    f_def = e.fit(g, Yd).f.cpu().numpy()
+    f_sm = e.fit(g, Yd, stan_faithful=True).f.cpu().numpy()
+    rel = (f_def - f_sm) / np.abs(f_sm)
+    assert int(np.sum(rel > 1e-6)) == 0, (np.flatnonzero(rel > 1e-6), float(rel.max()))

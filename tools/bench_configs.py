@@ -37,6 +37,10 @@ def main():
                     help="series of the Stan-faithful (stan_map) run that estimates the "
                          "algorithmic evaluation count E (0: skip)")
     ap.add_argument("--lib", default=None, help="load this engine library instead (A/B runs)")
+    ap.add_argument("--vs-stan-map", type=int, default=None,
+                    help="1: after the timed region refit every chunk with fit_mode stan_map "
+                         "(Stan's full rules + polish) and count series whose default fit ends "
+                         "worse (north_star's objective bar); default on for configs 3 and 4")
     ap.add_argument("--opt", action="append", default=[],
                     help="pf_fit_opts override name=value (repeatable), e.g. polish_lag_ratio=0.1")
     args = ap.parse_args()
@@ -189,13 +193,39 @@ def main():
                          "when the engine runs fewer evaluations than Stan (warm-up hand-off to the "
                          "polish) — a frac above 1 is credit for skipped evaluations, not hardware "
                          "rate; frac_performed is the rate on the evaluations actually run")}
+    # north_star's objective bar against Stan's own optimum: the default fit vs
+    # fit_mode stan_map (Stan's full termination rules, then the polish) on
+    # the same batch, series by series (untimed)
+    vs = None
+    if (args.vs_stan_map if args.vs_stan_map is not None else int(args.config in (3, 4))):
+        worse6 = worse9 = better6 = 0
+        maxrel = -np.inf
+        n_cmp = 0
+        t1 = time.perf_counter()
+        for k in range(len(chunks)):
+            fm = eng.fit(grid, Yd[k], cap=None if capd is None else capd[k], stan_faithful=True).f
+            f = stats[k][2]
+            ok = torch.isfinite(f) & torch.isfinite(fm)
+            rel = ((f - fm) / fm.abs())[ok]
+            worse6 += int((rel > 1e-6).sum().item())
+            worse9 += int((rel > 1e-9).sum().item())
+            better6 += int((rel < -1e-6).sum().item())
+            maxrel = max(maxrel, float(rel.max().item()) if rel.numel() else -np.inf)
+            n_cmp += int(ok.sum().item())
+            print(f"stan_map comparison chunk {k + 1}/{len(chunks)}", file=sys.stderr, flush=True)
+        vs = {"n_compared": n_cmp, "worse_than_stan_map_1e-6": worse6, "worse_than_stan_map_1e-9": worse9,
+              "better_than_stan_map_1e-6": better6, "max_rel": maxrel,
+              "stan_map_refit_s": time.perf_counter() - t1,
+              "note": "default fit's objective vs fit_mode stan_map (Stan's full L-BFGS rules + the "
+                      "certified polish) on the same series; north_star: no worse than Stan's optimum "
+                      "within 1e-6 relative"}
     stats = [(ne.double().mean().item(), (st == 70).double().mean().item()) for ne, st, _, _ in stats]
     res = {"metric": "series fit+forecast/sec", "config_index": args.config, "value": n / el,
            "unit": "series/s", "n_gpus": 1, "seconds": el, "workload": work, "chunk": chunk,
            "kernels_ms_total": kern, "tile_min_series": args.tile_min, "opt": args.opt,
            "n_eval_mean": float(np.mean([s[0] for s in stats])),
            "map_certified": float(np.mean([s[1] for s in stats])),
-           "roofline": roof, "uncertified": tail,
+           "roofline": roof, "uncertified": tail, "vs_stan_map": vs,
            "data": "synthetic (SURVEY.md §8d generators)"}
     print(json.dumps(res))
 

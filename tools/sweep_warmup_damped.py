@@ -1,0 +1,67 @@
+"""Diagnostic: with the polish's LM-damped first step, how short can the
+Stan warm-up before the hand-off be and still end every series in Stan's
+basin?  4 generator seeds x n series (1826 days): fit_mode stan_map once per
+seed (the bar), then the default fit at each (lbfgs_warmup, lbfgs_warmup_evals)
+cap: series worse than stan_map by > 1e-6 / 1e-9 relative, mean / max
+evaluations, the fit's kernel time (HIP events), and at n = 500 the
+configs[1]-shaped launch time.
+    python tools/sweep_warmup_damped.py [n] [out.json]"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+
+import distributed_forecasting_amd as dfa
+from distributed_forecasting_amd import synthetic
+from distributed_forecasting_amd.engine import ProphetConfig
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+out_path = sys.argv[2] if len(sys.argv) > 2 else None
+SEEDS = [dict(config_index=1), dict(config_index=2), dict(seed=1001), dict(seed=1002)]
+CAPS = [(60, 90), (50, 75), (45, 68), (40, 60), (30, 45), (20, 30)]
+e = dfa.Engine(0, ProphetConfig.reference())
+ds = synthetic.daily_dates()
+seasons = e.config.seasons(int(ds[0]), int(ds[-1]), int(ds[1] - ds[0]))
+g = dfa.build_grid(ds, seasons, start_ns=int(ds[0]), t_scale_ns=int(ds[-1] - ds[0]))
+
+
+def timed_fit(Yd, **kw):
+    torch.cuda.synchronize()
+    e.ctx.set_timing(True)
+    fit = e.fit(g, Yd, **kw)
+    torch.cuda.synchronize()
+    ms = sum(v for k, v, _ in e.ctx.read_timings() if k.startswith("k_fit") or k.startswith("k_polish"))
+    e.ctx.set_timing(False)
+    return fit, ms
+
+
+res = {"n": n, "caps": {}}
+for W, WE in CAPS:
+    res["caps"][f"{W}/{WE}"] = {"worse_1e-6": 0, "worse_1e-9": 0, "ms": [], "ms_500": [],
+                                "n_eval_mean": [], "n_eval_max": 0, "uncertified": 0}
+for gen in SEEDS:
+    Y = synthetic.sales_matrix(n, ds, **gen)
+    Yd = torch.zeros((n, g.T_pad), dtype=torch.float64, device="cuda")
+    Yd[:, :g.T] = torch.from_numpy(Y).cuda()
+    fm = e.fit(g, Yd, stan_faithful=True).f.cpu().numpy()
+    for W, WE in CAPS:
+        r = res["caps"][f"{W}/{WE}"]
+        fit, ms = timed_fit(Yd, lbfgs_warmup=W, lbfgs_warmup_evals=WE)
+        rel = (fit.f.cpu().numpy() - fm) / np.abs(fm)
+        r["worse_1e-6"] += int(np.sum(rel > 1e-6))
+        r["worse_1e-9"] += int(np.sum(rel > 1e-9))
+        r["uncertified"] += int((fit.status != 70).sum().item())
+        r["ms"].append(round(ms, 3))
+        r["n_eval_mean"].append(float(fit.n_eval.double().mean()))
+        r["n_eval_max"] = max(r["n_eval_max"], int(fit.n_eval.max()))
+        # the headline's launch shape: 500 series, one fused launch
+        _, ms5 = timed_fit(Yd[:500].contiguous(), lbfgs_warmup=W, lbfgs_warmup_evals=WE)
+        r["ms_500"].append(round(ms5, 3))
+        print(gen, W, WE, int(np.sum(rel > 1e-6)), round(ms, 2), round(ms5, 3), flush=True)
+print(json.dumps(res))
+if out_path:
+    with open(out_path, "w") as fh:
+        json.dump(res, fh, indent=1)
