@@ -117,7 +117,7 @@ typedef struct {
    * first (the reference's behaviour), then polish.  lbfgs_warmup_evals > 0
    * also ends a warm-up pass once it has used that many evaluations (at the
    * next accepted iterate, or inside a line search at the last accepted
-   * iterate once 10 more were used).  Defaults: 60 iterations, 90
+   * iterate once 10 more were used).  Defaults: 45 iterations, 68
    * evaluations.                                                           */
   int32_t lbfgs_warmup, lbfgs_warmup_evals;
   /* engine: batches of at least tile_min_series series run the first L-BFGS
