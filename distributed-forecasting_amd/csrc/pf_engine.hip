@@ -2320,7 +2320,8 @@ void pf_default_fit_opts(pf_fit_opts *o) {
   o->tile_min_series = 2048;
   o->polish_max_lag = 4;
   o->polish_lag_ratio = 1e-2;
-  o->polish_lam0 = 1e-4;    // damped first polish step (tools/diag_basin_floor.py)
+  o->polish_lam0 = 1e-2;    // damped first polish step (tools/diag_basin_floor.py)
+  if (const char *e = getenv("PF_POLISH_LAM0")) o->polish_lam0 = atof(e);   // diagnostic override
 }
 
 int pf_num_changepoints(int T, int n_changepoints, double changepoint_range) {

@@ -136,7 +136,7 @@ typedef struct {
    * (one Levenberg-Marquardt-damped step; later steps undamped unless a
    * non-positive pivot asks for damping).  An undamped first Newton step from
    * the warm-up hand-off can jump to a neighbouring, worse local optimum of
-   * the non-convex MAP objective.  Default 1e-4; 0 = undamped.             */
+   * the non-convex MAP objective.  Default 1e-2; 0 = undamped.             */
   double polish_lam0;
 } pf_fit_opts;
 

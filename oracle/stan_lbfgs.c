@@ -877,7 +877,7 @@ int orc_polish_cfg(const orc_problem *pb, double *theta, int max_it, int damp, d
  * non-convex MAP objective (tools/diag_basin_commit.py: the polish from Stan
  * iteration 60 lands 3e-5 .. 5e-4 above the MAP that the polish from
  * iterations 50 or 70 reaches); one damped step keeps it in the basin. */
-#define ORC_POLISH_LAM0 1e-4
+#define ORC_POLISH_LAM0 1e-2
 int orc_polish_ex(const orc_problem *pb, double *theta, int max_it, int damp, double *f_out,
                   int *n_newton, int *n_eval, int *n_solve, int *cert_out) {
     return orc_polish_cfg(pb, theta, max_it, damp, damp ? ORC_POLISH_LAM0 : 0.0, f_out, n_newton, n_eval,

@@ -174,7 +174,7 @@ def hessian_fd(pb: po.Problem, theta, h=1e-6):
     return H
 
 
-POLISH_LAM0 = 1e-4   # stan_lbfgs.c ORC_POLISH_LAM0 = pf_default_fit_opts().polish_lam0
+POLISH_LAM0 = 1e-2   # stan_lbfgs.c ORC_POLISH_LAM0 = pf_default_fit_opts().polish_lam0
 
 
 def polish(pb: po.Problem, theta, max_it=20, damp=False, return_cert=False, lam0=None,
