@@ -62,7 +62,7 @@ class PfFitOpts(ctypes.Structure):
                 ("max_iter", i32), ("history", i32), ("polish", i32), ("polish_max_iter", i32),
                 ("lbfgs_warmup", i32), ("lbfgs_warmup_evals", i32), ("tile_min_series", i32),
                 ("polish_max_lag", i32), ("polish_lag_ratio", ctypes.c_double),
-                ("polish_lam0", ctypes.c_double)]
+                ("polish_lam0", ctypes.c_double), ("lbfgs_warmup_ls_slack", i32)]
 
 
 class PfPredictArgs(ctypes.Structure):

@@ -535,8 +535,7 @@ __device__ __forceinline__ PV<PW> pv_zero() {
 
 // a warm-up pass (pf_fit_opts.lbfgs_warmup_evals > 0) ends at its next accepted
 // iterate once it has used that many evaluations, or inside a line search at
-// the last accepted iterate once it has used PF_WARM_LS_SLACK more
-#define PF_WARM_LS_SLACK 10
+// the last accepted iterate once it has used pf_fit_opts.lbfgs_warmup_ls_slack more
 
 struct FitKArgs {
   int T, Tp, K, S, growth, P, NB;
@@ -1430,7 +1429,7 @@ __device__ __forceinline__ bool lbfgs_step(const pf_fit_opts &o, LbLds<PW> &L, i
         state = LB_TRY;
         break;
       case LB_TRY:
-        if (o.lbfgs_warmup_evals > 0 && z.n_eval >= o.lbfgs_warmup_evals + PF_WARM_LS_SLACK) {
+        if (o.lbfgs_warmup_evals > 0 && z.n_eval >= o.lbfgs_warmup_evals + o.lbfgs_warmup_ls_slack) {
           // warm-up pass out of evaluations inside a line search: end it at
           // the last accepted iterate (the polish takes it from there)
           z.ret = PF_ST_MAXIT; state = LB_DONE; return false;
@@ -1476,7 +1475,7 @@ __device__ __forceinline__ bool lbfgs_step(const pf_fit_opts &o, LbLds<PW> &L, i
         break;
       }
       case LB_ZOOM_ITER: {
-        if (o.lbfgs_warmup_evals > 0 && z.n_eval >= o.lbfgs_warmup_evals + PF_WARM_LS_SLACK) {
+        if (o.lbfgs_warmup_evals > 0 && z.n_eval >= o.lbfgs_warmup_evals + o.lbfgs_warmup_ls_slack) {
           z.ret = PF_ST_MAXIT; state = LB_DONE; return false;
         }
         z.zit++;
@@ -2321,6 +2320,7 @@ void pf_default_fit_opts(pf_fit_opts *o) {
   o->polish_max_lag = 4;
   o->polish_lag_ratio = 1e-2;
   o->polish_lam0 = 1e-2;    // damped first polish step (tools/diag_basin_floor.py)
+  o->lbfgs_warmup_ls_slack = 10;
   if (const char *e = getenv("PF_POLISH_LAM0")) o->polish_lam0 = atof(e);   // diagnostic override
 }
 

@@ -138,6 +138,10 @@ typedef struct {
    * the warm-up hand-off can jump to a neighbouring, worse local optimum of
    * the non-convex MAP objective.  Default 1e-2; 0 = undamped.             */
   double polish_lam0;
+  /* engine warm-up: inside a line search the pass ends (at the last accepted
+   * iterate) once it has used lbfgs_warmup_evals + lbfgs_warmup_ls_slack
+   * evaluations.  Default 10.                                              */
+  int32_t lbfgs_warmup_ls_slack;
 } pf_fit_opts;
 
 /* component blocks pf_predict can report (seasonalities, holidays, ...) */

@@ -21,7 +21,7 @@ from distributed_forecasting_amd.engine import ProphetConfig
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 out_path = sys.argv[2] if len(sys.argv) > 2 else None
 SEEDS = [dict(config_index=1), dict(config_index=2), dict(seed=1001), dict(seed=1002)]
-CAPS = [(60, 90), (50, 75), (45, 68), (40, 60), (30, 45), (20, 30)]
+CAPS = [(45, 68, 10), (45, 68, 4), (45, 64, 4), (40, 60, 10), (40, 60, 4), (40, 56, 2), (35, 52, 4)]
 e = dfa.Engine(0, ProphetConfig.reference())
 ds = synthetic.daily_dates()
 seasons = e.config.seasons(int(ds[0]), int(ds[-1]), int(ds[1] - ds[0]))
@@ -39,17 +39,17 @@ def timed_fit(Yd, **kw):
 
 
 res = {"n": n, "caps": {}}
-for W, WE in CAPS:
-    res["caps"][f"{W}/{WE}"] = {"worse_1e-6": 0, "worse_1e-9": 0, "ms": [], "ms_500": [],
+for W, WE, SL in CAPS:
+    res["caps"][f"{W}/{WE}/{SL}"] = {"worse_1e-6": 0, "worse_1e-9": 0, "ms": [], "ms_500": [],
                                 "n_eval_mean": [], "n_eval_max": 0, "uncertified": 0}
 for gen in SEEDS:
     Y = synthetic.sales_matrix(n, ds, **gen)
     Yd = torch.zeros((n, g.T_pad), dtype=torch.float64, device="cuda")
     Yd[:, :g.T] = torch.from_numpy(Y).cuda()
     fm = e.fit(g, Yd, stan_faithful=True).f.cpu().numpy()
-    for W, WE in CAPS:
-        r = res["caps"][f"{W}/{WE}"]
-        fit, ms = timed_fit(Yd, lbfgs_warmup=W, lbfgs_warmup_evals=WE)
+    for W, WE, SL in CAPS:
+        r = res["caps"][f"{W}/{WE}/{SL}"]
+        fit, ms = timed_fit(Yd, lbfgs_warmup=W, lbfgs_warmup_evals=WE, lbfgs_warmup_ls_slack=SL)
         rel = (fit.f.cpu().numpy() - fm) / np.abs(fm)
         r["worse_1e-6"] += int(np.sum(rel > 1e-6))
         r["worse_1e-9"] += int(np.sum(rel > 1e-9))
@@ -58,9 +58,10 @@ for gen in SEEDS:
         r["n_eval_mean"].append(float(fit.n_eval.double().mean()))
         r["n_eval_max"] = max(r["n_eval_max"], int(fit.n_eval.max()))
         # the headline's launch shape: 500 series, one fused launch
-        _, ms5 = timed_fit(Yd[:500].contiguous(), lbfgs_warmup=W, lbfgs_warmup_evals=WE)
+        _, ms5 = timed_fit(Yd[:500].contiguous(), lbfgs_warmup=W, lbfgs_warmup_evals=WE,
+                           lbfgs_warmup_ls_slack=SL)
         r["ms_500"].append(round(ms5, 3))
-        print(gen, W, WE, int(np.sum(rel > 1e-6)), round(ms, 2), round(ms5, 3), flush=True)
+        print(gen, W, WE, SL, int(np.sum(rel > 1e-6)), round(ms, 2), round(ms5, 3), flush=True)
 print(json.dumps(res))
 if out_path:
     with open(out_path, "w") as fh:
