@@ -2314,13 +2314,13 @@ void pf_default_fit_opts(pf_fit_opts *o) {
   o->history = 5;
   o->polish = 1;
   o->polish_max_iter = 100;  // Newton steps (damped logistic fits from far away need up to ~52)
-  o->lbfgs_warmup = 45;       // with the damped first polish step (tools/sweep_warmup_damped.py)
-  o->lbfgs_warmup_evals = 68;  // also end a warm-up pass at 68 evaluations
+  o->lbfgs_warmup = 40;       // with the damped first polish step (tools/sweep_warmup_damped.py)
+  o->lbfgs_warmup_evals = 60;  // also end a warm-up pass at 60 evaluations
   o->tile_min_series = 2048;
   o->polish_max_lag = 4;
   o->polish_lag_ratio = 1e-2;
   o->polish_lam0 = 1e-2;    // damped first polish step (tools/diag_basin_floor.py)
-  o->lbfgs_warmup_ls_slack = 10;
+  o->lbfgs_warmup_ls_slack = 4;
   if (const char *e = getenv("PF_POLISH_LAM0")) o->polish_lam0 = atof(e);   // diagnostic override
 }
 

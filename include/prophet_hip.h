@@ -117,7 +117,7 @@ typedef struct {
    * first (the reference's behaviour), then polish.  lbfgs_warmup_evals > 0
    * also ends a warm-up pass once it has used that many evaluations (at the
    * next accepted iterate, or inside a line search at the last accepted
-   * iterate once 10 more were used).  Defaults: 45 iterations, 68
+   * iterate once lbfgs_warmup_ls_slack more were used).  Defaults: 40 iterations, 60
    * evaluations.                                                           */
   int32_t lbfgs_warmup, lbfgs_warmup_evals;
   /* engine: batches of at least tile_min_series series run the first L-BFGS
@@ -140,7 +140,7 @@ typedef struct {
   double polish_lam0;
   /* engine warm-up: inside a line search the pass ends (at the last accepted
    * iterate) once it has used lbfgs_warmup_evals + lbfgs_warmup_ls_slack
-   * evaluations.  Default 10.                                              */
+   * evaluations.  Default 4.                                               */
   int32_t lbfgs_warmup_ls_slack;
 } pf_fit_opts;
 
