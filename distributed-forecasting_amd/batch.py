@@ -233,8 +233,7 @@ def _dense(A, n: int, T: int, T_pad: int, dev) -> torch.Tensor:
     if isinstance(A, torch.Tensor):
         out[:, :T] = A[:, :T].to(dev, torch.float64)
     else:
-        out[:, :T] = torch.from_numpy(np.array(np.broadcast_to(
-            np.asarray(A, np.float64), (n, T)))).to(dev)
+        out[:, :T] = E._to_device_async(np.broadcast_to(np.asarray(A, np.float64), (n, T)), dev)
     return out
 
 
@@ -249,8 +248,8 @@ class FittedBatch:
         self.fit_ds = fit_ds
         self.series_ids = None
         if series_ids is not None:
-            self.series_ids = torch.from_numpy(np.ascontiguousarray(series_ids, dtype=np.int32)) \
-                .to(fit.theta.device)
+            self.series_ids = E._to_device_async(np.asarray(series_ids, dtype=np.int32),
+                                                 fit.theta.device)
 
     @property
     def n(self) -> int:
@@ -363,7 +362,7 @@ class FittedBatch:
         check_record_config(rec, engine.config)
         dev = torch.device("cuda", engine.device)
         sel = slice(None) if rows is None else np.asarray(rows)
-        theta = torch.from_numpy(np.ascontiguousarray(rec["theta"][sel])).to(dev)
+        theta = E._to_device_async(rec["theta"][sel], dev)
         n = theta.shape[0]
         seasons = [(str(a), float(b), int(c)) for a, b, c in
                    zip(rec["season_names"], rec["season_periods"], rec["season_orders"])]
@@ -374,10 +373,10 @@ class FittedBatch:
             raise ValueError(f"record theta has {theta.shape[1]} columns; its grid needs "
                              f"3 + S + K = {3 + S + K}")
         spec = GridSpec(seasons, int(rec["start_ns"]), int(rec["t_scale_ns"]),
-                        torch.from_numpy(np.ascontiguousarray(rec["t_change"])).to(dev), hol)
+                        E._to_device_async(rec["t_change"], dev), hol)
 
         def _t(name, dtype):
-            return torch.from_numpy(np.ascontiguousarray(rec[name][sel]).astype(dtype)).to(dev)
+            return E._to_device_async(rec[name][sel].astype(dtype), dev)
 
         fit = E.FitResult(spec, theta, _t("y_scale", np.float64), _t("f", np.float64),
                           _t("f", np.float64), _t("status", np.int32),
@@ -401,8 +400,8 @@ class RaggedFittedBatch:
         self.row0 = np.concatenate(([0], np.cumsum(sizes))).astype(np.int64)
         self.series_ids = None
         if series_ids is not None:
-            self.series_ids = torch.from_numpy(np.ascontiguousarray(series_ids, dtype=np.int32)) \
-                .to(fit.theta.device)
+            self.series_ids = E._to_device_async(np.asarray(series_ids, dtype=np.int32),
+                                                 fit.theta.device)
 
     @property
     def n(self) -> int:
@@ -474,7 +473,7 @@ class RaggedFittedBatch:
             for b in range(len(self.buckets)):
                 c = np.asarray(cap[b], np.float64)
                 ch[self.row0[b]:self.row0[b + 1], :c.shape[1]] = c
-            capd = torch.from_numpy(ch).to(self.fit.theta.device)
+            capd = E._to_device_async(ch, self.fit.theta.device)
         out = eng.predict(self.fit, fg, n_samples=n_samples, seed=seed, components=components,
                           series_id=self.series_ids, cap=capd)
         return [len(d) for d in ds_list], out

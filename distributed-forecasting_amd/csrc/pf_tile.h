@@ -1032,7 +1032,16 @@ __global__ __launch_bounds__(PF_TNW * 64, 1) void k_fit_tile(FitKArgs a, int n) 
     }
   }
   __syncthreads();
-  if (sidx >= 0) tile_publish<MODE, KP>(a, sm, j, g);
+  if (sidx < 0) {
+    // an empty slot (last tile, n % 16 != 0) still runs the row pass: give
+    // it a finite model (k = 1, every other parameter 0; k != 0 keeps the
+    // logistic offsets' ratios k_s / k_{s+1} finite) once
+    constexpr int TV = TileTr<MODE, KP>::TV;
+    for (int p = g; p < TV; p += 16) sm.xq[(size_t)j * TV + p] = (p == 0) ? 1.0 : 0.0;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  tile_publish<MODE, KP>(a, sm, j, g);
   __syncthreads();
   {
     const unsigned long long any = __ballot(sidx >= 0);

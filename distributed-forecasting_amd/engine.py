@@ -222,7 +222,7 @@ def _device_dates(ds_ns: np.ndarray, dev) -> torch.Tensor:
             # one kernel: exact int64 arithmetic, start + k * step
             return torch.arange(int(ds_ns[0]), int(ds_ns[0]) + step * T, step, dtype=torch.int64,
                                 device=dev)
-    return torch.from_numpy(ds_ns).to(dev)
+    return _to_device_async(ds_ns, dev)
 
 
 def build_grid(ds_ns: np.ndarray, seasons, *, start_ns: int, t_scale_ns: int,
@@ -269,7 +269,7 @@ def build_grid(ds_ns: np.ndarray, seasons, *, start_ns: int, t_scale_ns: int,
     cp_first = torch.empty(S, dtype=torch.int32, device=dev)
     extra = None
     if n_extra:
-        extra = torch.from_numpy(np.ascontiguousarray(holiday_columns(holidays, ds_ns))).to(dev)
+        extra = _to_device_async(holiday_columns(holidays, ds_ns), dev)
     rc = ctx.lib.pf_build_grid(ctx.h, _ptr(ds_d), T, Tp, int(start_ns), int(t_scale_ns), sp,
                                len(seasons), _ptr(extra), n_extra, ncp, float(changepoint_range), _ptr(t),
                                _ptr(XT), _ptr(tc), _ptr(cp_idx), _ptr(seg), _ptr(cp_first), S,
@@ -570,8 +570,7 @@ class Engine:
                 sig[:, grid.K - nh:] = np.asarray(h.prior_scales, np.float64)[None, :]
             else:
                 sig[:, grid.K - nh:] = vec(holidays_prior_scale, cfg.holidays_prior_scale)[:, None]
-        return (torch.from_numpy(np.ascontiguousarray(tau)).to(dev),
-                torch.from_numpy(sig).to(dev))
+        return _to_device_async(tau, dev), _to_device_async(sig, dev)
 
     def problem(self, grid: DeviceGrid, y_scaled: torch.Tensor, n: int,
                 cap_scaled: torch.Tensor | None = None, priors=None) -> L.PfProblem:

@@ -214,7 +214,10 @@ class ForecastStoreItemModel:
         ``model_input``.  Returns [ds, store, item, yhat, yhat_upper,
         yhat_lower]; each group's rows sorted by ds (Prophet.predict order).
         Logistic-growth stores need a ``cap`` column (UPSTREAM predict)."""
-        from .training import dense_frame
+        return self._predict(model_input, True)
+
+    def _predict(self, model_input: pd.DataFrame, guess: bool) -> pd.DataFrame:
+        from .training import dense_guess
         for c in ("ds", "store", "item"):
             if c not in model_input:
                 raise ValueError(f"model_input must have column {c!r}")
@@ -239,13 +242,22 @@ class ForecastStoreItemModel:
 
         # group the groups: same record + same (sorted) dates -> one launch
         jobs = {}
-        dense = dense_frame(model_input, ["store", "item"], value="cap" if logistic else None)
+        # grouped input in key order, every group on the same dates: no
+        # per-group date handling (the usual scoring frame).  The layout is
+        # read off the first group; the O(rows) checks run while the GPU works
+        dense = dense_guess(model_input, ["store", "item"], value="cap" if logistic else None) \
+            if guess else None
+        verify = None
         if dense is not None:
-            # grouped input in key order, every group on the same dates: no
-            # per-group date handling (the usual scoring frame)
-            gkeys, ds0, capm = dense
+            gkeys, ds0, capm, verify = dense
+            verify.start()
             for g, key in enumerate(map(tuple, gkeys.tolist())):
-                name, row = lookup(key)
+                try:
+                    name, row = lookup(key)
+                except KeyError:
+                    if verify():
+                        raise
+                    return self._predict(model_input, False)
                 j = jobs.setdefault(name, (ds0, [], [], []))
                 j[1].append(row)
                 j[2].append(key)
@@ -294,6 +306,8 @@ class ForecastStoreItemModel:
             done = torch.cuda.Event()
             done.record(torch.cuda.current_stream(dev))
             launched.append((ds, keys, Tf, host, done))
+        if verify is not None and not verify():
+            return self._predict(model_input, False)   # not the dense layout
         frames = []
         for ds, keys, Tf, host, done in launched:
             n = len(keys)

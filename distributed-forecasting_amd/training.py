@@ -147,27 +147,40 @@ def group_frame(df: pd.DataFrame, keys):
     return np.stack([c[first] for c in cols], axis=1), [order[s:e] for s, e in zip(starts, ends)]
 
 
-def dense_frame(df: pd.DataFrame, keys, value: str | None = "y"):
-    """The sales table's usual layout without per-group work: the frame is
-    grouped, its groups come in increasing key order, every group holds the
-    same strictly increasing dates and no ``value`` is NaN.  Returns (group
-    keys [n, k] int64, dates [T] int64 ns, values [n, T] float64 — a view of
-    the ``value`` column, None if ``value`` is None) or None when any of that
-    does not hold (then ``group_frame`` + ``bucket_groups`` run).  Vectorised
-    checks only: O(rows) with no Python loop over groups."""
+def dense_guess(df: pd.DataFrame, keys, value: str | None = "y"):
+    """The O(groups + dates) half of ``dense_frame``: reads the layout off the
+    first group (its length T = the first key change) and checks what that
+    costs nothing to check (T divides the rows, strictly increasing dates in
+    the first group, strictly increasing group keys at every T-th row).
+    Returns (group keys [n, k] int64, dates [T] int64 ns, values [n, T]
+    float64 view or None, verify) or None; ``verify`` (a RowChecks: start()
+    submits, verify() waits) runs the O(rows) checks (every group on the first group's dates, keys constant inside each
+    group, no NaN value) and must return True before the guess is used for
+    anything a caller can observe.  Callers launch the GPU work on the guess
+    and verify while it runs."""
     N = len(df)
     if N == 0 or (value is not None and value not in df):
         return None
     cols = [df[k].to_numpy() for k in keys]
     if any(c.dtype.kind not in "iu" for c in cols):
         return None
-    ch = cols[0][1:] != cols[0][:-1]
-    for c in cols[1:]:
-        ch |= c[1:] != c[:-1]
-    brk = np.flatnonzero(ch) + 1
-    n = brk.shape[0] + 1
-    T = N // n
-    if T < 2 or n * T != N or (n > 1 and not np.array_equal(brk, np.arange(1, n) * T)):
+    # first key change: scan growing prefixes (a sorted table finds it in
+    # the first chunk)
+    T, m = N, 4096
+    while True:
+        lim = min(N, m)
+        ch = np.zeros(lim - 1, bool)
+        for c in cols:
+            ch |= c[1:lim] != c[0]
+        hit = np.flatnonzero(ch)
+        if hit.shape[0]:
+            T = int(hit[0]) + 1
+            break
+        if lim == N:
+            break
+        m *= 8
+    n = N // T
+    if T < 2 or n * T != N:
         return None
     gkeys = np.stack([c[::T].astype(np.int64) for c in cols], axis=1)
     if n > 1:
@@ -187,15 +200,65 @@ def dense_frame(df: pd.DataFrame, keys, value: str | None = "y"):
     if ds.dtype != np.dtype("datetime64[ns]"):
         ds = ds.astype("datetime64[ns]")
     dsi = ds.view(np.int64).reshape(n, T)
-    ds0 = dsi[0]
-    if not bool(np.all(ds0[1:] > ds0[:-1])) or (n > 1 and not bool((dsi[1:] == ds0).all())):
+    ds0 = np.array(dsi[0])
+    if not bool(np.all(ds0[1:] > ds0[:-1])):
         return None
-    if value is None:
-        return gkeys, np.array(ds0), None
-    y = df[value].to_numpy(np.float64)
-    if bool(np.isnan(y).any()):
+    Y = df[value].to_numpy(np.float64).reshape(n, T) if value is not None else None
+
+    def rows_ok(a: int, b: int) -> bool:
+        for c in cols:
+            c2 = c.reshape(n, T)[a:b]
+            if not np.array_equal(c2.min(axis=1), c2.max(axis=1)):
+                return False
+        if not bool((dsi[max(a, 1):b] == ds0).all()):
+            return False
+        return Y is None or not bool(np.isnan(Y[a:b]).any())
+    return gkeys, ds0, Y, RowChecks(rows_ok, n)
+
+
+class RowChecks:
+    """The O(rows) half of a layout check, run over group ranges on a small
+    thread pool (numpy releases the GIL in its loops): ``start()`` submits
+    the ranges and returns at once, so the checks overlap the caller's GPU
+    launches and output assembly; calling the object waits and returns True
+    when every range passed."""
+    _pool = None
+    CHUNKS = 4
+
+    def __init__(self, fn, n: int):
+        self.fn, self.n, self.futs = fn, n, None
+
+    @classmethod
+    def pool(cls):
+        if cls._pool is None:
+            from concurrent.futures import ThreadPoolExecutor
+            cls._pool = ThreadPoolExecutor(max_workers=cls.CHUNKS, thread_name_prefix="pf-rowcheck")
+        return cls._pool
+
+    def start(self) -> "RowChecks":
+        if self.futs is None:
+            k = min(self.CHUNKS, self.n)
+            cut = [self.n * i // k for i in range(k + 1)]
+            self.futs = [self.pool().submit(self.fn, a, b) for a, b in zip(cut[:-1], cut[1:])]
+        return self
+
+    def __call__(self) -> bool:
+        self.start()
+        return all(f.result() for f in self.futs)
+
+
+def dense_frame(df: pd.DataFrame, keys, value: str | None = "y"):
+    """The sales table's usual layout without per-group work: the frame is
+    grouped, its groups come in increasing key order, every group holds the
+    same strictly increasing dates and no ``value`` is NaN.  Returns (group
+    keys [n, k] int64, dates [T] int64 ns, values [n, T] float64 — a view of
+    the ``value`` column, None if ``value`` is None) or None when any of that
+    does not hold (then ``group_frame`` + ``bucket_groups`` run).  Vectorised
+    checks only: O(rows) with no Python loop over groups."""
+    g = dense_guess(df, keys, value)
+    if g is None or not g[3]():
         return None
-    return gkeys, np.array(ds0), y.reshape(n, T)
+    return g[:3]
 
 
 def _empty_frame(cols, keys):
@@ -208,7 +271,8 @@ def forecast_store_items(df: pd.DataFrame, keys=("store", "item"), *, periods: i
                          freq="d", config: E.ProphetConfig | None = None, device=None,
                          seed: int = 0, params_store=None, rank: int = 0,
                          world_size: int = 1, return_fits: bool = False,
-                         cv_metrics: bool = False, return_metrics: bool = False):
+                         cv_metrics: bool = False, return_metrics: bool = False,
+                         _guess: bool = True):
     """Batched equivalent of
     ``df.groupBy(*keys).applyInPandas(forecast_store_item, schema)``.
 
@@ -233,10 +297,13 @@ def forecast_store_items(df: pd.DataFrame, keys=("store", "item"), *, periods: i
     eng = get_engine(cfg, device)
     dev = torch.device("cuda", eng.device)
     cols = ["ds"] + keys + ["y", "yhat", "yhat_upper", "yhat_lower"]
-    dense = dense_frame(df, keys)
+    # the sorted sales table: one bucket, no per-group Python.  The layout is
+    # read off the first group and the O(rows) checks run while the GPU works
+    # (dense_guess); a frame that fails them is redone by the general path
+    dense = dense_guess(df, keys) if _guess else None
+    verify = None
     if dense is not None:
-        # one bucket, no per-group Python (the sorted sales table)
-        gkeys, ds0, Y = dense
+        gkeys, ds0, Y, verify = dense
         if world_size > 1:
             mine = np.flatnonzero(B.shard_of(gkeys, world_size) == rank)
             gkeys, Y = gkeys[mine], Y[mine]
@@ -291,6 +358,19 @@ def forecast_store_items(df: pd.DataFrame, keys=("store", "item"), *, periods: i
                     eng, bk.fit_ds, Yc, seasons=fb.fit.grid.seasons,
                     series_ids=B.series_id(bkeys), seed=seed))
         launched.append((bks, futs, row0, host, done, subs, mets))
+
+    if verify is not None:
+        # started after the launches: the row checks would otherwise compete
+        # with the pinned staging copy of Y for memory bandwidth
+        verify.start()
+    if verify is not None and not verify():
+        # not the dense layout after all: the launches above are dropped
+        # (nothing was stored) and the general path runs
+        return forecast_store_items(df, keys, periods=periods, freq=freq, config=config,
+                                    device=device, seed=seed, params_store=params_store,
+                                    rank=rank, world_size=world_size, return_fits=return_fits,
+                                    cv_metrics=cv_metrics, return_metrics=return_metrics,
+                                    _guess=False)
 
     # phase 2: output columns (schema of 02_training.py:307); y is copied by
     # position from each group's frame (NaN past its rows)

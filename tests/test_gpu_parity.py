@@ -397,6 +397,19 @@ def test_params_store_and_pyfunc(eng, tmp_path):
     # same params, same RNG stream key (store, item) and seed -> identical output
     for k in ("yhat", "yhat_lower", "yhat_upper"):
         assert np.array_equal(a[k].values, b[k].values), k
+    # a frame whose first group looks dense but whose last group sits on other
+    # dates: the guessed launch is dropped and the general path serves it
+    fut2 = fut.copy()
+    last = (fut2.store == 2) & (fut2.item == 2)
+    fut2.loc[last, "ds"] = fut2.loc[last, "ds"] + pd.Timedelta(days=1)
+    out2 = model.predict(None, fut2)
+    assert len(out2) == len(fut2)
+    keep = ~((out2.store == 2) & (out2.item == 2))
+    o2 = out2[keep].sort_values(["store", "item", "ds"]).reset_index(drop=True)
+    b2 = b[~((b.store == 2) & (b.item == 2))].reset_index(drop=True)
+    assert np.array_equal(o2["ds"].values, b2["ds"].values)
+    assert np.array_equal(o2["yhat"].values, b2["yhat"].values)
+    assert np.array_equal(np.sort(out2.loc[~keep, "ds"].values), np.sort(fut2.loc[last, "ds"].values))
     dfa.register_model(model)
     one = fut[(fut.store == 1) & (fut.item == 2)].tail(90)
     r = dfa.predict_udf(one)

@@ -439,6 +439,42 @@ def test_dense_frame_fast_path_agrees_with_general_path():
     assert training.dense_frame(df.iloc[:0], ["store", "item"]) is None
 
 
+def test_dense_guess_defers_only_the_row_checks():
+    """training.dense_guess reads the layout off the first group; the layouts
+    only the O(rows) checks can tell apart pass the guess and fail verify()
+    (the callers then take the general path), the others fail the guess."""
+    df = synthetic.store_item_frame(3, 4, "2016-01-01", "2017-12-31")
+    gk, ds0, Y, verify = training.dense_guess(df, ["store", "item"])
+    assert verify() and np.array_equal(gk, training.dense_frame(df, ["store", "item"])[0])
+    T = len(ds0)
+    late = []
+    d = df.copy()
+    d.loc[5 * T + 3, "y"] = np.nan                        # NaN in a later group
+    late.append(d)
+    d = df.copy()
+    d.loc[4 * T + 7, "ds"] = d.loc[4 * T + 7, "ds"] + pd.Timedelta(hours=1)   # other dates
+    late.append(d)
+    d = df.copy()
+    d.loc[3 * T + 2, "item"] = d.loc[3 * T + 2, "item"] + 1                  # key split
+    late.append(d)
+    for d in late:
+        g = training.dense_guess(d, ["store", "item"])
+        assert g is not None and not g[3]()
+        assert training.dense_frame(d, ["store", "item"]) is None
+    # caught by the guess itself: rows not a multiple of T, unsorted first
+    # group, keys out of order
+    assert training.dense_guess(df.iloc[:-1].reset_index(drop=True), ["store", "item"]) is None
+    d = df.copy()
+    d.loc[1, "ds"], d.loc[2, "ds"] = df.loc[2, "ds"], df.loc[1, "ds"]
+    assert training.dense_guess(d, ["store", "item"]) is None
+    order = np.concatenate([np.arange(T, 2 * T), np.arange(T), np.arange(2 * T, len(df))])
+    assert training.dense_guess(df.iloc[order].reset_index(drop=True), ["store", "item"]) is None
+    # one group: T = all rows
+    one = df.iloc[:T].reset_index(drop=True)
+    g = training.dense_guess(one, ["store", "item"])
+    assert g[1].shape[0] == T and g[0].shape[0] == 1 and g[3]()
+
+
 def _legacy_store(path, recs):
     """A params store in the first record format (manifest 'records' list of
     bucket_NNNNNN.npz files, no 'format' key)."""
