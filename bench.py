@@ -30,7 +30,8 @@ barrier + synchronize, max over ranks):
   configs2_strong BASELINE configs[2]: 50,000 series x 1826 days in total,
                   hash-sharded over the N ranks (strong scaling), per-rank
                   counts reported
-roofline: the dominant kernel (k_fit_polish), timed with HIP events recorded by
+roofline: the dominant kernel (k_fit_forecast: fit + polish + each series' forecast
+rows and metrics in one launch; k_fit_polish when unfused), timed with HIP events recorded by
 the engine on the launch stream.  achieved = SURVEY §8d algorithmic FLOPs (the
 oracle Stan run's evaluation count E per series x 4T(F+2C)) / kernel time;
 achieved_performed = the evaluations the engine actually ran.
@@ -401,6 +402,20 @@ def main():
     fit, fg, out, met = unpack(r)
     total_series = sum_over_ranks(n)
     value = total_series * args.steps / elapsed
+    # the same step as separate launches (fit | K4 + K6 || K5 on a side
+    # stream): the per-kernel times of the forecast kernels, and the gain of
+    # the fused launch
+    ustep = dfa.ForecastStep(eng, ds, n, horizon=HORIZON, series_id=sid, metrics="fast", fuse=False)
+    ustep.set_inputs(Yd[:, :T])
+    el_unf, kern_unf, _ = timed(stepped(lambda: gather(ustep.run())), args.steps, args.warmup,
+                                ustep.engine.ctx, drain=drain)
+    try:
+        ustep.capture()
+        el_unf_g, _, _ = timed(stepped(lambda: gather(ustep.replay())), args.steps, args.warmup,
+                               ustep.engine.ctx, drain=drain)
+    except Exception:                       # capture unsupported: the eager figure
+        el_unf_g = el_unf
+    ustep.close()
 
     res = {
         "metric": "series fit+forecast/sec (1826d daily, 90d horizon, 1000-sample 95% intervals)",
@@ -430,6 +445,13 @@ def main():
                             "reference's cross-validation metrics (02_training.py:178-188: 3 fold "
                             "refits) are the dropin.forecast_store_items_cv and cv_on legs"},
         "launch": launch,
+        "fused": bool(fstep.fused),
+        "unfused": {"value": total_series * args.steps / el_unf_g, "unit": "series/s",
+                    "ms_per_step": el_unf_g / args.steps * 1e3, "kernels_ms": kern_unf,
+                    "note": "the same step as separate launches (k_fit_polish, then k_predict_det "
+                            "+ k_cv_metrics on the step's stream and k_predict_mc on a side "
+                            "stream), graph-replayed; the headline runs them as one launch "
+                            "(pf_fit_forecast, k_fit_forecast: bitwise the same outputs)"},
         "eager": {"value": total_series * args.steps / el_eager, "unit": "series/s",
                   "ms_per_step": el_eager / args.steps * 1e3,
                   "note": "the same step launched eagerly (Python + ctypes per launch); "
@@ -462,7 +484,7 @@ def main():
     E_all = np.array(man["E"], dtype=np.float64)
     E_mean = float(E_all.mean())
     evals = float(fit.n_eval.double().sum().item())
-    fit_kernel = "k_fit_polish" if "k_fit_polish" in kern_avg else "k_fit"
+    fit_kernel = next(k for k in ("k_fit_forecast", "k_fit_polish", "k_fit") if k in kern_avg)
     fit_s = kern_avg.get(fit_kernel, float("nan")) / 1e3
     # algorithmic work per series = E x 4T(F+2C), E = the
     # oracle's Stan-faithful evaluation count for that series (fixed per
@@ -495,14 +517,16 @@ def main():
                 "Stan run's evaluations E per series x 4T(F+2C)) / the fused fit+polish kernel's "
                 "time; frac_performed = the kernel-efficiency figure on the L-BFGS evaluations "
                 "the engine performed; traffic = HBM bytes per launch from rocprofv3 PMC "
-                "(profiles/pmc_k_fit.json)"}
+                "(profiles/pmc_k_fit.json).  k_fit_forecast also runs each series' forecast "
+                "rows and metrics (K4/K5/K6) after its fit: its time includes them, its FLOPs "
+                "count only the fit's (conservative)"}
     # K5 (the Monte-Carlo future rows, the longest forecast kernel) is
     # VALU-issue-bound work (Philox, Box-Muller, wave sorts): its roofline is
     # the vector-instruction issue rate, one wave64 VALU instruction per 2
     # cycles per SIMD (1024 SIMDs at 2.4 GHz), with the instruction count per
     # launch from rocprofv3 PMC (SQ_INSTS_VALU, profiles/pmc_k_predict_mc.json,
     # same launch shape) over the live kernel time
-    mc_ms = kern_avg.get("k_predict_mc")
+    mc_ms = kern_unf.get("k_predict_mc")
     mc_pmc = None
     mc_path = os.path.join(ROOT, "profiles", "pmc_k_predict_mc.json")
     if os.path.exists(mc_path):

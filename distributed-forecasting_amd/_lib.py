@@ -22,10 +22,11 @@ PF_ST_CONSTANT = 50
 EXPORTED = ["pf_ctx_create", "pf_ctx_destroy", "pf_last_error", "pf_default_fit_opts",
             "pf_num_changepoints", "pf_build_grid", "pf_prepare", "pf_objective_grad",
             "pf_fit", "pf_predict", "pf_set_timing", "pf_read_timings", "pf_cv_metrics",
-            "pf_hessian", "pf_prepare_ragged", "pf_build_grids", "pf_build_id"]
+            "pf_hessian", "pf_prepare_ragged", "pf_build_grids", "pf_build_id", "pf_fit_forecast"]
 PF_MAX_COMP = 32  # include/prophet_hip.h
 PF_INTERVAL = {"exact": 0, "sample": 1}
 PF_PREDICT_DET, PF_PREDICT_MC = 1, 2
+PF_FF_ONLY_FUSED = 1
 CV_METRICS = ["mse", "rmse", "mae", "mape", "smape", "coverage", "mdape"]
 
 
@@ -149,6 +150,9 @@ def load(path: str = LIB_PATH):
     lib.pf_fit.argtypes = [vp, ctypes.POINTER(PfProblem), ctypes.POINTER(PfFitOpts),
                            vp, vp, vp, vp, vp, vp, vp]
     lib.pf_predict.argtypes = [vp, ctypes.POINTER(PfPredictArgs), vp]
+    lib.pf_fit_forecast.argtypes = [vp, ctypes.POINTER(PfProblem), ctypes.POINTER(PfFitOpts),
+                                    vp, vp, vp, vp, vp, vp, ctypes.POINTER(PfPredictArgs),
+                                    ctypes.POINTER(PfCvArgs), ctypes.c_int, ctypes.POINTER(i32), vp]
     lib.pf_cv_metrics.argtypes = [vp, ctypes.POINTER(PfCvArgs), vp]
     lib.pf_set_timing.argtypes = [vp, ctypes.c_int]
     lib.pf_read_timings.argtypes = [vp, ctypes.POINTER(PfKernelTime), ctypes.c_int]

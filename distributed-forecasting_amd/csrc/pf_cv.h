@@ -75,13 +75,15 @@ __device__ __forceinline__ double cv_radix_select(const unsigned long long *keys
 // selects (ranks (n-1)/2 and n/2) over the APE bit patterns cached in LDS.
 #define PF_CV_INS_WAVES 4
 #define PF_CV_INS_CACHE 3072
-__global__ __launch_bounds__(PF_CV_INS_WAVES * 64) void k_cv_insample(CvKArgs a) {
-  __shared__ unsigned long long s_cache[PF_CV_INS_CACHE];
-  __shared__ double s_part[PF_CV_INS_WAVES][6];
-  __shared__ int s_hist[256];
-  __shared__ int s_bad;
+// One series' in-sample metrics by a block of PF_CV_INS_WAVES waves.  LDS:
+// s_cache [PF_CV_INS_CACHE] (MDAPE only), s_part [PF_CV_INS_WAVES][6],
+// s_hist [256], s_bad [1].  Waves other than 0 return after the block
+// barrier.  Shared by k_cv_insample and the fused forecast epilogue.
+__device__ __forceinline__ void cv_insample_block(const CvKArgs &a, int series, unsigned long long *s_cache,
+                                                  double (*s_part)[6], int *s_hist, int *s_bad_) {
+  int &s_bad = *s_bad_;
   constexpr int NT = PF_CV_INS_WAVES * 64;
-  const int series = blockIdx.x, lane = pf_lane(), wave = pf_wave(), tid = threadIdx.x;
+  const int lane = pf_lane(), wave = pf_wave(), tid = threadIdx.x;
   const double *y = a.y + (size_t)series * a.ld_y;
   const float *yh = a.yhat + (size_t)series * a.ld_f;
   const float *lo = a.ylo ? a.ylo + (size_t)series * a.ld_f : nullptr;
@@ -162,6 +164,17 @@ __global__ __launch_bounds__(PF_CV_INS_WAVES * 64) void k_cv_insample(CvKArgs a)
     m[PF_CV_COVERAGE] = lo ? t[4] / w : NAN;
     m[PF_CV_MDAPE] = (!anybad && !a.skip_mdape) ? (v0 + v1) * 0.5 : NAN;
   }
+}
+
+// the kernels live in the main unit only (the fit units use the device
+// functions above through the fused forecast epilogue)
+#if PF_MAIN
+__global__ __launch_bounds__(PF_CV_INS_WAVES * 64) void k_cv_insample(CvKArgs a) {
+  __shared__ unsigned long long s_cache[PF_CV_INS_CACHE];
+  __shared__ double s_part[PF_CV_INS_WAVES][6];
+  __shared__ int s_hist[256];
+  __shared__ int s_bad;
+  cv_insample_block(a, blockIdx.x, s_cache, s_part, s_hist, &s_bad);
 }
 
 __global__ __launch_bounds__(64) void k_cv_metrics(CvKArgs a) {
@@ -259,3 +272,4 @@ __global__ __launch_bounds__(64) void k_cv_metrics(CvKArgs a) {
     a.metrics[(size_t)series * PF_CV_NMETRICS + m] = v;
   }
 }
+#endif  // PF_MAIN

@@ -32,9 +32,7 @@
 #define PF_MAIN 1
 #endif
 
-#if PF_MAIN
 #include "pf_cv.h"
-#endif
 #include "pf_ostat.h"
 
 #ifndef M_PI
@@ -82,11 +80,71 @@ __device__ unsigned long long pf_dbg[32];
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)                  \
       atomicAdd(&pf_dbg[i], (unsigned long long)__builtin_amdgcn_s_memtime());   \
   } while (0)
+// every wave of every block (lane 0): path counters
+#define PF_COUNTW(i)                                                             \
+  do {                                                                           \
+    if (pf_lane() == 0) atomicAdd(&pf_dbg[i], 1ull);                             \
+  } while (0)
 #else
+#define PF_COUNTW(i) do { } while (0)
 #define PF_STAMP1(i) do { } while (0)
 #define PF_STAMP(i) do { } while (0)
 #define PF_COUNT(i) do { } while (0)
 #endif
+
+#if defined(PF_STAMPS) && !defined(PF_TIMELINE)
+#define PF_TIMELINE
+#endif
+// Diagnostic build only (-DPF_TIMELINE, tools/block_timeline.py): no other
+// instrumentation, so the timeline is the product kernel's.
+#ifdef PF_TIMELINE
+// per-block timeline of the fused launch: [start, fit end, end] s_memrealtime
+// (100 MHz, one clock for every XCD)
+// [3]: the first L-BFGS phase's end (the polish starts); blocks < 4096
+// [4] / [5]: the polish's Newton steps / exact Hessians (all passes, summed)
+// [6] / [7]: time in the polish's Hessian assembly / sweep-in (memrealtime ticks)
+// [8] / [9] / [10]: time in the QP (wave 0) / the polish's line-search
+// evaluations / the stash restore
+__device__ unsigned long long pf_blk[11][4096];
+#define PF_BLK(i)                                                                \
+  do {                                                                           \
+    if (threadIdx.x == 0 && blockIdx.x < 4096)                                   \
+      pf_blk[i][blockIdx.x] = (unsigned long long)__builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#define PF_RT() ((unsigned long long)__builtin_amdgcn_s_memrealtime())
+#define PF_BLKV(i, v)                                                            \
+  do {                                                                           \
+    if (threadIdx.x == 0 && blockIdx.x < 4096) pf_blk[i][blockIdx.x] += (unsigned long long)(v); \
+  } while (0)
+#else
+#define PF_BLK(i) do { } while (0)
+#define PF_BLKV(i, v) do { } while (0)
+#define PF_RT() 0ull
+#endif
+
+// Wave priorities.  Two fit workgroups share each CU and the SIMD arbiter
+// otherwise prefers the older one's waves, so the younger workgroup's serial
+// steps (one wave works, the other three wait at the next barrier) queue
+// behind the older one's row pass and its fit ends up to ~50% later
+// (tools/block_timeline.py).  Serial sections run at 3, the rest of a fit
+// at 1, and the fused forecast epilogue (k_fit_forecast) at 0: the critical
+// path first on every SIMD, the epilogue in the gaps the fits leave.
+__device__ __forceinline__ void pf_serial_prio(bool on) {
+#ifndef PF_NO_PRIO
+  if (on) __builtin_amdgcn_s_setprio(3);
+  else __builtin_amdgcn_s_setprio(1);
+#else
+  (void)on;
+#endif
+}
+__device__ __forceinline__ void pf_base_prio(int p) {
+#ifndef PF_NO_PRIO
+  if (p == 0) __builtin_amdgcn_s_setprio(0);
+  else __builtin_amdgcn_s_setprio(1);
+#else
+  (void)p;
+#endif
+}
 
 // diagnostic switch (environment): "1" enables
 static bool getenv_flag(const char *name) {
@@ -1806,6 +1864,9 @@ __device__ __forceinline__ void fit_body(const FitKArgs &a, int pass, const pf_f
     eval_rows<NW, KMAX, O0, O1, O2, MODE>(a, sm);
     __syncthreads();
     if (pf_wave() == 0) {
+      // the workgroup's serial section: the other workgroup on this CU is
+      // in its row pass meanwhile (pf_serial_prio)
+      pf_serial_prio(true);
       double fq, gpq;
       PV<PW> gq, pkc;
 #pragma unroll
@@ -1819,6 +1880,7 @@ __device__ __forceinline__ void fit_body(const FitKArgs &a, int pass, const pf_f
       const bool need = lbfgs_advance(o, L, xq, gq, gpq, bad);
       if (need) publish_theta<NW, KMAX, MODE>(a, sm, xq);
       if (lane == 0) sm.flag[0] = need ? 1 : 0;
+      pf_serial_prio(false);
     }
     __syncthreads();
     PF_STAMP(5);
@@ -1873,6 +1935,7 @@ __device__ __forceinline__ void polish_body(const FitKArgs &a) {
   if (bad) return;
   int n_eval = 1, n_newton = 0;  // polish evaluations are not counted in n_eval[]
   const bool cert = polish_run<NW, KMAX, O0, O1, O2, MODE>(a, sm, x, f, g, n_eval, n_newton);
+  PF_BLKV(4, n_newton);
   if (threadIdx.x < 64) {
 #pragma unroll
     for (int h = 0; h < PW; ++h)
@@ -1988,6 +2051,7 @@ __device__ __forceinline__ void fit_polish_passes(const FitKArgs &a) {
     const bool warm = ps < 2;
     fit_phase<NW, KMAX, O0, O1, O2, MODE>(a, ps, warm ? W : a.o.max_iter, warm);
     __syncthreads();
+    if (ps == 0) PF_BLK(3);
     polish_phase<NW, KMAX, O0, O1, O2, MODE>(a);
     __syncthreads();
     const int st = __builtin_amdgcn_readfirstlane(__atomic_load_n(&a.status[blockIdx.x], __ATOMIC_RELAXED));
@@ -2217,6 +2281,90 @@ __global__ __launch_bounds__(256) void k_predict_det(PredKArgs a0) {
 }
 
 #include "pf_mc.h"
+
+// ============================================================================
+// K3 + K4 + K5 + K6 in one launch (pf_fit_forecast): each series' forecast
+// rows and in-sample metrics run in its own fit workgroup as soon as its fit
+// + polish ends, so they fill the time the batch's slowest fits leave the
+// other CUs idle instead of waiting for the whole fit launch to drain.  The
+// rows are computed by the very device functions k_predict_det /
+// k_predict_mc / k_cv_insample run (same arithmetic, same RNG streams keyed by
+// (series id, row, sample)): the outputs are bitwise those of the separate
+// launches.  Exact intervals, one grid, the warm-up hand-off fit path.
+// ============================================================================
+struct FuseArgs {
+  PredKArgs p;
+  CvKArgs cv;
+  int metrics;  // run K6 (in-sample: one group of every history row)
+};
+// what pf_fit_forecast asks of the fit launcher: fuse when the fit takes the
+// fused fit + polish path (done = 1); only = 1: launch nothing otherwise
+struct FuseReq {
+  const FuseArgs *args;
+  int only;
+  int done;
+};
+// epilogue LDS, from the dynamic LDS base (the fit's layout is dead by then)
+struct FuseSmem {
+  static constexpr size_t cp_off = (sizeof(PredSeries) + 15) & ~(size_t)15;
+  static constexpr size_t meta_off = cp_off + PF_MC_CPCAP * sizeof(float2);
+  static constexpr size_t buf_off = meta_off + 64 * PF_NQ * sizeof(uint32_t);
+  static constexpr size_t wsum_off = buf_off + PF_MC_WAVES * 4 * 64 * sizeof(float);
+  static constexpr size_t r0_off = wsum_off + PF_MC_WAVES * sizeof(double);
+  // K6 runs after the Monte-Carlo rows: its APE cache reuses s_cp
+  static constexpr size_t cache_off = cp_off;
+  static constexpr size_t part_off = r0_off + 16;
+  static constexpr size_t hist_off = part_off + PF_CV_INS_WAVES * 6 * sizeof(double);
+  static constexpr size_t bad_off = hist_off + 256 * sizeof(int);
+  static constexpr size_t bytes = bad_off + 16;
+};
+static_assert(PF_CV_INS_CACHE * sizeof(unsigned long long) <= PF_MC_CPCAP * sizeof(float2),
+              "K6 cache must fit the changepoint slots it aliases");
+
+template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
+__global__ __launch_bounds__(NW * 64, FitOcc<KMAX>::W) void k_fit_forecast(FitKArgs a, FuseArgs e) {
+  static_assert(NW == PF_MC_WAVES && NW == PF_CV_INS_WAVES, "fused epilogue: one block shape");
+  PF_BLK(0);
+  pf_base_prio(1);
+  fit_polish_passes<NW, KMAX, O0, O1, O2, MODE>(a);
+  __syncthreads();   // theta of this series written (wave 0), the fit's LDS dead
+  PF_BLK(1);
+  pf_base_prio(0);
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  PredSeries &ps = *reinterpret_cast<PredSeries *>(smem_raw);
+  float2 *s_cp = reinterpret_cast<float2 *>(smem_raw + FuseSmem::cp_off);
+  uint32_t *s_meta = reinterpret_cast<uint32_t *>(smem_raw + FuseSmem::meta_off);
+  float *s_buf = reinterpret_cast<float *>(smem_raw + FuseSmem::buf_off);
+  double *s_wsum = reinterpret_cast<double *>(smem_raw + FuseSmem::wsum_off);
+  int *s_r0 = reinterpret_cast<int *>(smem_raw + FuseSmem::r0_off);
+  const int series = blockIdx.x;
+  const PredKArgs &pa = e.p;
+  const uint32_t sid = pa.series_id ? pa.series_id[series] : (uint32_t)series;
+  if (threadIdx.x == 0) *s_r0 = pa.Tf;
+  pred_setup(pa, series, ps);
+  __syncthreads();
+  // K4: every row's point forecast (+ components), the deterministic rows'
+  // exact intervals
+  const double t_max = pa.t[pa.Tf - 1];
+  for (int row = threadIdx.x; row < pa.Tf; row += NW * 64)
+    det_row(pa, ps, series, sid, row, t_max, e.p.comp_col0, e.p.comp_ncol);
+  // K5: the random-trend rows' Monte-Carlo intervals
+  if (pa.N > 0) {
+    if (pa.tr) mc_block<true>(pa, ps, series, sid, 0, 1, s_cp, s_meta, s_buf, s_wsum, s_r0);
+    else mc_block<false>(pa, ps, series, sid, 0, 1, s_cp, s_meta, s_buf, s_wsum, s_r0);
+  }
+  if (!e.metrics) {
+    __syncthreads();
+    PF_BLK(2);
+    return;
+  }
+  __syncthreads();   // this series' yhat / intervals written
+  cv_insample_block(e.cv, series, reinterpret_cast<unsigned long long *>(smem_raw + FuseSmem::cache_off),
+                    reinterpret_cast<double (*)[6]>(smem_raw + FuseSmem::part_off),
+                    reinterpret_cast<int *>(smem_raw + FuseSmem::hist_off),
+                    reinterpret_cast<int *>(smem_raw + FuseSmem::bad_off));
+  PF_BLK(2);
+}
 
 #if PF_MAIN
 // ============================================================================
@@ -2568,9 +2716,10 @@ FitKArgs make_fit_args(const pf_problem *pb) {
 enum { PF_LAUNCH_OBJGRAD = 0, PF_LAUNCH_FIT = 1, PF_LAUNCH_HESSIAN = 2 };
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
 int launch_fitlike_impl(pf_ctx *ctx, int what, const FitKArgs &a, int n, hipStream_t st, double *H_out,
-                        size_t smem, size_t smem_p);
+                        size_t smem, size_t smem_p, FuseReq *fz);
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
-int launch_fitlike(pf_ctx *ctx, int what, const FitKArgs &a, int n, hipStream_t st, double *H_out) {
+int launch_fitlike(pf_ctx *ctx, int what, const FitKArgs &a, int n, hipStream_t st, double *H_out,
+                   FuseReq *fz) {
   // the polish handles K <= 48 (three 16-column beta blocks) and 2 + S <= 32
   constexpr bool HAS_POLISH = KMAX <= 48;
   const size_t smem = FitSmem<NW, KMAX, MODE>::bytes(a.TQ, a.P, a.S, false);
@@ -2587,11 +2736,11 @@ int launch_fitlike(pf_ctx *ctx, int what, const FitKArgs &a, int n, hipStream_t 
       a2.hstash = 1;
     }
   }
-  return launch_fitlike_impl<NW, KMAX, O0, O1, O2, MODE>(ctx, what, a2, n, st, H_out, smem, smem_p);
+  return launch_fitlike_impl<NW, KMAX, O0, O1, O2, MODE>(ctx, what, a2, n, st, H_out, smem, smem_p, fz);
 }
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
 int launch_fitlike_impl(pf_ctx *ctx, int what, const FitKArgs &a, int n, hipStream_t st, double *H_out,
-                        size_t smem, size_t smem_p) {
+                        size_t smem, size_t smem_p, FuseReq *fz) {
   constexpr bool HAS_POLISH = KMAX <= 48;
   if (smem > 160 * 1024) return set_err(ctx, "fit: series too long for the LDS budget");
   if (what == PF_LAUNCH_HESSIAN) {
@@ -2651,6 +2800,23 @@ int launch_fitlike_impl(pf_ctx *ctx, int what, const FitKArgs &a, int n, hipStre
     }
     if (npass == 3 && !tile && !getenv_flag("PF_SPLIT_POLISH")) {
       if constexpr (HAS_POLISH) {
+        if (fz) {
+          // fused forecast epilogue: the fit's LDS, grown to the epilogue's
+          // when needed only while that keeps the workgroups per CU
+          const size_t sf0 = smem_p > smem ? smem_p : smem;
+          const size_t sf = sf0 > FuseSmem::bytes ? sf0 : FuseSmem::bytes;
+          const size_t cap = (FitOcc<KMAX>::W >= 2 && sf0 <= 80 * 1024) ? 80 * 1024 : 160 * 1024;
+          if (sf <= cap) {
+            auto kff = k_fit_forecast<NW, KMAX, O0, O1, O2, MODE>;
+            PF_HIP(ctx, hipFuncSetAttribute((const void *)kff, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            (int)sf));
+            PF_TIMED_LAUNCH(ctx, "k_fit_forecast", n, st, kff, dim3(n), dim3(NW * 64), sf, st, a, *fz->args);
+            PF_HIP(ctx, hipGetLastError());
+            fz->done = 1;
+            return 0;
+          }
+          if (fz->only) return 0;
+        }
         auto kfp = k_fit_polish<NW, KMAX, O0, O1, O2, MODE>;
         PF_HIP(ctx, hipFuncSetAttribute((const void *)kfp, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         (int)(smem_p > smem ? smem_p : smem)));
@@ -2660,6 +2826,7 @@ int launch_fitlike_impl(pf_ctx *ctx, int what, const FitKArgs &a, int n, hipStre
         return 0;
       }
     }
+    if (fz && fz->only) return 0;   // not the fused path: the caller launches the parts
     for (int ps = 0; ps < npass; ++ps) {
       FitKArgs b = a;
       b.o.max_iter = caps[ps];
@@ -2724,7 +2891,8 @@ int launch_fitlike_impl(pf_ctx *ctx, int what, const FitKArgs &a, int n, hipStre
 // the main unit uses the instances the fit units define
 #define PF_EXTERN_INST(G, K, O0, O1, O2, M)                                               \
   extern template int launch_fitlike<PF_FIT_NW, K, O0, O1, O2, M>(pf_ctx *, int, const FitKArgs &, \
-                                                                  int, hipStream_t, double *);
+                                                                  int, hipStream_t, double *,      \
+                                                                  FuseReq *);
 PF_FIT_INSTANCES(PF_EXTERN_INST)
 #endif
 #endif
@@ -2738,7 +2906,7 @@ namespace {
 //   (34, 10,3,4, MULT) — sub-daily data (yearly + weekly + daily 4; config 5)
 //   dense fallbacks KMAX 32 / 61 (any K <= KMAX), features read from X^T.
 int dispatch_fitlike(pf_ctx *ctx, int fit, const FitKArgs &a, int n, const int32_t *orders, int mode,
-                     hipStream_t st, double *H_out = nullptr) {
+                     hipStream_t st, double *H_out = nullptr, FuseReq *fz = nullptr) {
   const bool o1030 = orders[0] == 10 && orders[1] == 3 && orders[2] == 0;
   const bool o1034 = orders[0] == 10 && orders[1] == 3 && orders[2] == 4;
   constexpr int LG = PF_MODE_LOGI, WD = PF_MODE_WIDE;
@@ -2747,32 +2915,32 @@ int dispatch_fitlike(pf_ctx *ctx, int fit, const FitKArgs &a, int n, const int32
   // (P <= 72: two parameter words per lane) — SURVEY.md §8d configs[4]
   if (o1030 && a.K > 26 && a.K <= 36 && mode == MODE_MULT) {
     if (a.growth == PF_GROWTH_LOGISTIC)
-      return launch_fitlike<PF_FIT_NW, 36, 10, 3, 0, MODE_MULT | LG>(ctx, fit, a, n, st, H_out);
-    return launch_fitlike<PF_FIT_NW, 36, 10, 3, 0, MODE_MULT>(ctx, fit, a, n, st, H_out);
+      return launch_fitlike<PF_FIT_NW, 36, 10, 3, 0, MODE_MULT | LG>(ctx, fit, a, n, st, H_out, fz);
+    return launch_fitlike<PF_FIT_NW, 36, 10, 3, 0, MODE_MULT>(ctx, fit, a, n, st, H_out, fz);
   }
   if (o1034 && a.K > 34 && a.K <= 44 && mode == MODE_MULT) {
     if (a.growth == PF_GROWTH_LOGISTIC)
-      return launch_fitlike<PF_FIT_NW, 44, 10, 3, 4, MODE_MULT | LG | WD>(ctx, fit, a, n, st, H_out);
-    return launch_fitlike<PF_FIT_NW, 44, 10, 3, 4, MODE_MULT | WD>(ctx, fit, a, n, st, H_out);
+      return launch_fitlike<PF_FIT_NW, 44, 10, 3, 4, MODE_MULT | LG | WD>(ctx, fit, a, n, st, H_out, fz);
+    return launch_fitlike<PF_FIT_NW, 44, 10, 3, 4, MODE_MULT | WD>(ctx, fit, a, n, st, H_out, fz);
   }
   if (a.P > 64) return set_err(ctx, "fit: P > 64 is supported for yearly+weekly+daily (10,3,4) plus <= 10 extra columns, multiplicative");
   if (a.growth == PF_GROWTH_LOGISTIC) {
     if (o1030 && a.K == 26 && mode == MODE_MULT)
-      return launch_fitlike<PF_FIT_NW, 26, 10, 3, 0, MODE_MULT | LG>(ctx, fit, a, n, st, H_out);
+      return launch_fitlike<PF_FIT_NW, 26, 10, 3, 0, MODE_MULT | LG>(ctx, fit, a, n, st, H_out, fz);
     if (o1034 && a.K == 34 && mode == MODE_MULT)
-      return launch_fitlike<PF_FIT_NW, 34, 10, 3, 4, MODE_MULT | LG>(ctx, fit, a, n, st, H_out);
-    if (a.K <= 32) return launch_fitlike<PF_FIT_NW, 32, 0, 0, 0, MODE_MIXED | LG>(ctx, fit, a, n, st, H_out);
+      return launch_fitlike<PF_FIT_NW, 34, 10, 3, 4, MODE_MULT | LG>(ctx, fit, a, n, st, H_out, fz);
+    if (a.K <= 32) return launch_fitlike<PF_FIT_NW, 32, 0, 0, 0, MODE_MIXED | LG>(ctx, fit, a, n, st, H_out, fz);
     return set_err(ctx, "fit: logistic growth supports K <= 32, or yearly+weekly+daily (K = 34) multiplicative");
   }
   if (o1030 && a.K == 26) {
-    if (mode == MODE_MULT) return launch_fitlike<PF_FIT_NW, 26, 10, 3, 0, MODE_MULT>(ctx, fit, a, n, st, H_out);
-    if (mode == MODE_ADD) return launch_fitlike<PF_FIT_NW, 26, 10, 3, 0, MODE_ADD>(ctx, fit, a, n, st, H_out);
-    return launch_fitlike<PF_FIT_NW, 26, 10, 3, 0, MODE_MIXED>(ctx, fit, a, n, st, H_out);
+    if (mode == MODE_MULT) return launch_fitlike<PF_FIT_NW, 26, 10, 3, 0, MODE_MULT>(ctx, fit, a, n, st, H_out, fz);
+    if (mode == MODE_ADD) return launch_fitlike<PF_FIT_NW, 26, 10, 3, 0, MODE_ADD>(ctx, fit, a, n, st, H_out, fz);
+    return launch_fitlike<PF_FIT_NW, 26, 10, 3, 0, MODE_MIXED>(ctx, fit, a, n, st, H_out, fz);
   }
   if (o1034 && a.K == 34 && mode == MODE_MULT)
-    return launch_fitlike<PF_FIT_NW, 34, 10, 3, 4, MODE_MULT>(ctx, fit, a, n, st, H_out);
-  if (a.K <= 32) return launch_fitlike<PF_FIT_NW, 32, 0, 0, 0, MODE_MIXED>(ctx, fit, a, n, st, H_out);
-  if (a.K <= 61) return launch_fitlike<PF_FIT_NW, 61, 0, 0, 0, MODE_MIXED>(ctx, fit, a, n, st, H_out);
+    return launch_fitlike<PF_FIT_NW, 34, 10, 3, 4, MODE_MULT>(ctx, fit, a, n, st, H_out, fz);
+  if (a.K <= 32) return launch_fitlike<PF_FIT_NW, 32, 0, 0, 0, MODE_MIXED>(ctx, fit, a, n, st, H_out, fz);
+  if (a.K <= 61) return launch_fitlike<PF_FIT_NW, 61, 0, 0, 0, MODE_MIXED>(ctx, fit, a, n, st, H_out, fz);
   return set_err(ctx, "fit: K > 61 not supported");
 }
 
@@ -2911,7 +3079,8 @@ int pf_hessian(pf_ctx *ctx, const pf_problem *pb, const double *theta, double *H
                           (hipStream_t)stream, H);
 }
 
-int pf_predict(pf_ctx *ctx, const pf_predict_args *p, void *stream) {
+// pf_predict's checks and kernel arguments (shared with pf_fit_forecast)
+static int make_pred_args(pf_ctx *ctx, const pf_predict_args *p, PredKArgs &a) {
   if (!p) return set_err(ctx, "pf_predict: NULL args");
   if (p->n_samples < 0 || p->n_samples > 64 * PF_NQ) return set_err(ctx, "pf_predict: n_samples must be in [0, 1024]");
   const int P = 3 + p->fg.S + p->fg.K;
@@ -2926,8 +3095,6 @@ int pf_predict(pf_ctx *ctx, const pf_predict_args *p, void *stream) {
   if ((p->trend != nullptr) != (p->trend_lower != nullptr) ||
       (p->trend != nullptr) != (p->trend_upper != nullptr))
     return set_err(ctx, "pf_predict: trend/trend_lower/trend_upper must be all set or all NULL");
-  if (p->n_series == 0) return 0;
-  PredKArgs a;
   memset(&a, 0, sizeof a);
   a.n_series = p->n_series;
   a.growth = p->growth;
@@ -3011,6 +3178,15 @@ int pf_predict(pf_ctx *ctx, const pf_predict_args *p, void *stream) {
     return set_err(ctx, "pf_predict: interval_method must be PF_INTERVAL_EXACT or PF_INTERVAL_SAMPLE");
   const int parts = p->parts == 0 ? (PF_PREDICT_DET | PF_PREDICT_MC) : p->parts;
   if (parts & ~(PF_PREDICT_DET | PF_PREDICT_MC)) return set_err(ctx, "pf_predict: bad parts");
+  return 0;
+}
+
+int pf_predict(pf_ctx *ctx, const pf_predict_args *p, void *stream) {
+  PredKArgs a;
+  const int rc = make_pred_args(ctx, p, a);
+  if (rc) return rc;
+  if (p->n_series == 0) return 0;
+  const int parts = p->parts == 0 ? (PF_PREDICT_DET | PF_PREDICT_MC) : p->parts;
   const dim3 grid((a.Tf + 256 * PF_DET_RPT - 1) / (256 * PF_DET_RPT), a.n_series);
   if (parts & PF_PREDICT_DET) {
     PF_TIMED_LAUNCH(ctx, "k_predict_det", grid.x * grid.y, (hipStream_t)stream,
@@ -3062,7 +3238,8 @@ int pf_predict(pf_ctx *ctx, const pf_predict_args *p, void *stream) {
   return 0;
 }
 
-int pf_cv_metrics(pf_ctx *ctx, const pf_cv_args *p, void *stream) {
+// pf_cv_metrics's checks and kernel arguments (shared with pf_fit_forecast)
+static int make_cv_args(pf_ctx *ctx, const pf_cv_args *p, CvKArgs &a) {
   if (!p) return set_err(ctx, "pf_cv_metrics: NULL args");
   if (p->n_series < 0 || p->n_rows < 1 || p->n_groups < 1 || p->n_groups > PF_CV_GMAX ||
       p->window < 1)
@@ -3076,8 +3253,6 @@ int pf_cv_metrics(pf_ctx *ctx, const pf_cv_args *p, void *stream) {
     return set_err(ctx, "pf_cv_metrics: group_start NULL needs window = n_rows (one group)");
   if ((p->yhat_lower == nullptr) != (p->yhat_upper == nullptr))
     return set_err(ctx, "pf_cv_metrics: yhat_lower/yhat_upper must be both set or both NULL");
-  if (p->n_series == 0) return 0;
-  CvKArgs a;
   a.n_series = p->n_series;
   a.n_rows = p->n_rows;
   a.n_groups = p->n_groups;
@@ -3091,6 +3266,14 @@ int pf_cv_metrics(pf_ctx *ctx, const pf_cv_args *p, void *stream) {
   a.ylo = p->yhat_lower;
   a.yhi = p->yhat_upper;
   a.metrics = p->metrics;
+  return 0;
+}
+
+int pf_cv_metrics(pf_ctx *ctx, const pf_cv_args *p, void *stream) {
+  CvKArgs a;
+  const int rc = make_cv_args(ctx, p, a);
+  if (rc) return rc;
+  if (p->n_series == 0) return 0;
   if (p->n_groups == 1 && p->window == p->n_rows)   // one group of every row: in-sample
     PF_TIMED_LAUNCH(ctx, "k_cv_metrics", p->n_series, (hipStream_t)stream, k_cv_insample,
                     dim3(p->n_series), dim3(PF_CV_INS_WAVES * 64), 0, (hipStream_t)stream, a);
@@ -3101,6 +3284,62 @@ int pf_cv_metrics(pf_ctx *ctx, const pf_cv_args *p, void *stream) {
   return 0;
 }
 
+int pf_fit_forecast(pf_ctx *ctx, const pf_problem *pb, const pf_fit_opts *opts, double *theta_inout,
+                    double *f_out, double *f_stan, int32_t *status, int32_t *n_iter, int32_t *n_eval,
+                    const pf_predict_args *pred, const pf_cv_args *cv, int flags, int32_t *fused,
+                    void *stream) {
+  if (fused) *fused = 0;
+  int rc = check_problem(ctx, pb);
+  if (rc) return rc;
+  if (!opts || !theta_inout || !f_out || !f_stan || !status || !n_iter || !n_eval)
+    return set_err(ctx, "pf_fit_forecast: NULL fit output");
+  if (flags & ~PF_FF_ONLY_FUSED) return set_err(ctx, "pf_fit_forecast: bad flags");
+  FuseArgs fa;
+  memset(&fa, 0, sizeof fa);
+  rc = make_pred_args(ctx, pred, fa.p);
+  if (rc) return rc;
+  if (cv) {
+    rc = make_cv_args(ctx, cv, fa.cv);
+    if (rc) return rc;
+    fa.metrics = 1;
+  }
+  if (pred->n_series != pb->n_series || pred->theta != theta_inout || (cv && cv->n_series != pb->n_series))
+    return set_err(ctx, "pf_fit_forecast: the forecast and metrics must cover the fitted series (theta = theta_inout)");
+  if (pb->n_series == 0) return 0;
+  const hipStream_t st = (hipStream_t)stream;
+  // one launch: one grid, exact intervals, every forecast part, in-sample metrics
+  const bool can = pb->n_grids == 0 && pred->n_grids == 0 && fa.p.method == PF_INTERVAL_EXACT &&
+                   (pred->parts == 0 || pred->parts == (PF_PREDICT_DET | PF_PREDICT_MC)) &&
+                   (!cv || (cv->n_groups == 1 && cv->window == cv->n_rows)) && !getenv_flag("PF_NO_FUSE");
+  const bool only = (flags & PF_FF_ONLY_FUSED) != 0;
+  if (!can && only) return 0;
+  FuseReq fz{&fa, only ? 1 : 0, 0};
+  FitKArgs a = make_fit_args(pb);
+  a.theta = theta_inout;
+  a.f_out = f_out;
+  a.f_stan = f_stan;
+  a.status = status;
+  a.n_iter = n_iter;
+  a.n_eval = n_eval;
+  a.o = *opts;
+  const bool maybe_tile = opts->tile_min_series >= 0 && pb->n_series >= opts->tile_min_series &&
+                          pb->grid.K <= 48 && pb->n_grids == 0 && !pb->tau_series &&
+                          !pb->sigmas_series;
+  rc = prepare_fit_scratch(ctx, a, st, maybe_tile, pb->n_grids);
+  if (rc) return rc;
+  rc = dispatch_fitlike(ctx, PF_LAUNCH_FIT, a, pb->n_series, pb->fourier_orders, mode_of(pb), st, nullptr,
+                        can ? &fz : nullptr);
+  if (rc) return rc;
+  if (fz.done) {
+    if (fused) *fused = 1;
+    return 0;
+  }
+  if (can && only) return 0;   // the fit took another path: nothing launched
+  rc = pf_predict(ctx, pred, stream);
+  if (rc) return rc;
+  return cv ? pf_cv_metrics(ctx, cv, stream) : 0;
+}
+
 }  // extern "C"
 #endif  // PF_MAIN (dispatch, C ABI part 2)
 
@@ -3109,7 +3348,7 @@ int pf_cv_metrics(pf_ctx *ctx, const pf_cv_args *p, void *stream) {
 #if defined(PF_TU) && PF_TU >= 1
 #define PF_INST_BODY(K, O0, O1, O2, M)                                                     \
   template int launch_fitlike<PF_FIT_NW, K, O0, O1, O2, M>(pf_ctx *, int, const FitKArgs &, int, \
-                                                           hipStream_t, double *);
+                                                           hipStream_t, double *, FuseReq *);
 #define PF_SKIP(K, O0, O1, O2, M)
 #define PF_EMIT_1 PF_SKIP
 #define PF_EMIT_2 PF_SKIP
@@ -3147,6 +3386,15 @@ PF_FIT_INSTANCES(PF_DEF_INST)
 // diagnostic stamps read-back: defined in the unit whose kernels write the
 // stamps (each split unit has its own device copy of pf_dbg) — the
 // reference-layout fit unit, or the single unit
+#if defined(PF_TIMELINE) && (!defined(PF_TU) || PF_TU == 1)
+extern "C" int pf_debug_blocks(unsigned long long *out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pf_blk), sizeof(unsigned long long) * 11 * 4096) != hipSuccess) return -2;
+  unsigned long long *z = (unsigned long long *)calloc(11 * 4096, sizeof(unsigned long long));
+  const hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(pf_blk), z, sizeof(unsigned long long) * 11 * 4096);
+  free(z);
+  return e == hipSuccess ? 0 : -2;
+}
+#endif
 #if defined(PF_STAMPS) && (!defined(PF_TU) || PF_TU == 1)
 extern "C" int pf_debug_stamps(unsigned long long *out, int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pf_dbg), sizeof(unsigned long long) * 32) != hipSuccess) return -2;

@@ -165,9 +165,10 @@ __device__ __forceinline__ void wave_tail_select(const float (&v)[PF_NQ], const 
       bool ok = true;
 #pragma unroll
       for (int s = 0; s < NS; ++s) ok = ok && M[s] >= kk[s] + 2 && M[s] <= 64;
-      if (ok) break;
+      if (ok) { PF_COUNTW(13); break; }
     }
   }
+  PF_COUNTW(14);
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     int w = pre[s] - cl[s];
@@ -196,6 +197,7 @@ __device__ __forceinline__ void wave_tail_select(const float (&v)[PF_NQ], const 
       o0[s] = (k < M[s]) ? readlane_f32(c[s], k) : U[s];
       o1[s] = (k + 1 < M[s]) ? readlane_f32(c[s], k + 1) : U[s];
     } else {
+      PF_COUNTW(25);
       for (int want = 0; want < 2; ++want) {
         uint32_t lo = 0u, hi = 0xFFFFFFFFu;
         while (lo < hi) {
@@ -506,26 +508,21 @@ __device__ __forceinline__ void mc_rows(const PredKArgs &a, const PredSeries &ps
   }
 }
 
-template <int KMAX, bool TR>
-__global__ __launch_bounds__(PF_MC_WAVES * 64) void k_predict_mc(PredKArgs a0) {
-  PredKArgs a = a0;
-  if (a0.grid_of) bind_pred_grid(a, blockIdx.y);
+// One block's share of a series' Monte-Carlo rows (block bx of gdx over the
+// random rows), the series' PredSeries already set up in ps (pred_setup +
+// a block barrier).  LDS: s_cp [PF_MC_CPCAP], s_meta [64 PF_NQ], s_buf
+// [PF_MC_WAVES][4 * 64], s_wsum [PF_MC_WAVES], s_r0 [1].  A wave without rows
+// returns early (no block-level sync after the setup).  Shared by
+// k_predict_mc and the fused forecast epilogue (k_fit_forecast).
+template <bool TR>
+__device__ __forceinline__ void mc_block(const PredKArgs &a, const PredSeries &ps, int series, uint32_t sid,
+                                         int bx, int gdx, float2 *s_cp, uint32_t *s_meta, float *s_buf,
+                                         double *s_wsum, int *s_r0) {
   constexpr int NT = PF_MC_WAVES * 64;
   constexpr int SPT = (64 * PF_NQ) / NT;  // samples per thread in the setup
-  __shared__ PredSeries ps;
-  __shared__ float2 s_cp[PF_MC_CPCAP];     // (tau_c, delta), each sample's run in time order
-  __shared__ uint32_t s_meta[64 * PF_NQ];  // first slot | end << 13  (overflow: count)
-  __shared__ float s_buf[PF_MC_WAVES][4 * 64];
-  __shared__ double s_wsum[PF_MC_WAVES];
-  __shared__ int s_r0;
-  const int series = blockIdx.y, lane = pf_lane(), wave = pf_wave(), tid = threadIdx.x;
-  const uint32_t sid = a.series_id ? a.series_id[series] : (uint32_t)series;
+  const int lane = pf_lane(), wave = pf_wave(), tid = threadIdx.x;
   const int N = a.N;
-  PF_STAMP1(0);
-  if (tid == 0) s_r0 = a.Tf;
-  pred_setup(a, series, ps);
   const double t_max = a.t[a.Tf - 1];
-  __syncthreads();
   {
     // first random-trend row (rows sorted by t): independent loads, min
     int loc = a.Tf;
@@ -536,7 +533,7 @@ __global__ __launch_bounds__(PF_MC_WAVES * 64) void k_predict_mc(PredKArgs a0) {
         if (r < a.Tf && pred_row_random(a, a.t[r], t_max)) loc = min(loc, r);
       }
     }
-    if (loc < a.Tf) atomicMin(&s_r0, loc);
+    if (loc < a.Tf) atomicMin(s_r0, loc);
   }
   // ---- per-sample new changepoints, packed in time order
   const double lam = ps.lam;
@@ -584,16 +581,36 @@ __global__ __launch_bounds__(PF_MC_WAVES * 64) void k_predict_mc(PredKArgs a0) {
   }
   __syncthreads();
   PF_STAMP1(1);
-  const int r0 = s_r0;
+  const int r0 = *s_r0;
   const int nrows = a.Tf - r0;
   if (nrows <= 0) return;
-  const int nw = gridDim.x * PF_MC_WAVES;
+  const int nw = gdx * PF_MC_WAVES;
   const int rpw = (nrows + nw - 1) / nw;
-  const int row_b = r0 + (blockIdx.x * PF_MC_WAVES + wave) * rpw;
+  const int row_b = r0 + (bx * PF_MC_WAVES + wave) * rpw;
   const int row_e = min(row_b + rpw, a.Tf);
   if (row_b >= row_e) return;  // no block-level sync below
-  if (ovf) mc_rows<true, TR>(a, ps, s_cp, s_meta, s_buf[wave], series, sid, t_max, row_b, row_e);
-  else mc_rows<false, TR>(a, ps, s_cp, s_meta, s_buf[wave], series, sid, t_max, row_b, row_e);
+  float *buf = s_buf + wave * 4 * 64;
+  if (ovf) mc_rows<true, TR>(a, ps, s_cp, s_meta, buf, series, sid, t_max, row_b, row_e);
+  else mc_rows<false, TR>(a, ps, s_cp, s_meta, buf, series, sid, t_max, row_b, row_e);
+}
+
+template <int KMAX, bool TR>
+__global__ __launch_bounds__(PF_MC_WAVES * 64) void k_predict_mc(PredKArgs a0) {
+  PredKArgs a = a0;
+  if (a0.grid_of) bind_pred_grid(a, blockIdx.y);
+  __shared__ PredSeries ps;
+  __shared__ float2 s_cp[PF_MC_CPCAP];     // (tau_c, delta), each sample's run in time order
+  __shared__ uint32_t s_meta[64 * PF_NQ];  // first slot | end << 13  (overflow: count)
+  __shared__ float s_buf[PF_MC_WAVES][4 * 64];
+  __shared__ double s_wsum[PF_MC_WAVES];
+  __shared__ int s_r0;
+  const int series = blockIdx.y;
+  const uint32_t sid = a.series_id ? a.series_id[series] : (uint32_t)series;
+  PF_STAMP1(0);
+  if (threadIdx.x == 0) s_r0 = a.Tf;
+  pred_setup(a, series, ps);
+  __syncthreads();
+  mc_block<TR>(a, ps, series, sid, blockIdx.x, gridDim.x, s_cp, s_meta, &s_buf[0][0], s_wsum, &s_r0);
 }
 
 // ---- sample mode, deterministic-trend rows (the history: t <= 1, or every

@@ -566,6 +566,159 @@ __device__ __forceinline__ void sweep_in_free(const FitKArgs &a, FitSmem<NW, KMA
   __syncthreads();
 }
 
+// Block form of sweep_in_free: up to PF_SWEEP_BLK pivots K per round, in the
+// same order.  With B = A[K][K] (current values) and W = B^-1 A[K][:],
+//   A'[i][j] = A[i][j] - A[i][K] W[:][j]   (i, j not in K)
+//   A'[K][j] = A'[j][K] = W[:][j],  A'[K][K] = -B^-1,
+// which is the sequential sweep of K in exact arithmetic; B^-1 comes from the
+// sequential sweeps of the small block, so the positive-pivot checks are the
+// sequential ones.  Two barriers per round instead of two per pivot, and one
+// read + write of each matrix entry per round instead of per pivot.
+#ifndef PF_SWEEP_BLK
+#define PF_SWEEP_BLK 2
+#endif
+template <int NW, int KMAX, int MODE>
+__device__ __forceinline__ void sweep_in_free_blk(const FitKArgs &a, FitSmem<NW, KMAX, MODE> &sm,
+                                                  const PV<ModeTr<MODE>::PW> &gh, double c) {
+  constexpr int PW = ModeTr<MODE>::PW;
+  constexpr int BK = PF_SWEEP_BLK > 0 ? PF_SWEEP_BLK : 1;
+  const int lane = pf_lane(), wave = pf_wave();
+  const int P = __builtin_amdgcn_readfirstlane(a.P), S = __builtin_amdgcn_readfirstlane(a.S);
+  const int LD = __builtin_amdgcn_readfirstlane(sm.LD);
+  double *A = sm.U;
+  constexpr int RW = (64 * PW + NW - 1) / NW;  // rows per wave
+  const int r0 = wave * RW;
+  if (threadIdx.x == 0) sm.flag[1] = 0;
+  __syncthreads();
+  const bool isd = (lane >= 2 && lane < 2 + S);
+  const bool zero = isd && fabs(gh[0]) <= c;
+  unsigned long long fm[PW];
+  fm[0] = __ballot(lane < P && !zero);
+  if constexpr (PW > 1) fm[1] = __ballot(lane + 64 < P);
+  while (true) {
+    int ks[BK];
+    int nb = 0;
+#pragma unroll
+    for (int h0 = 0; h0 < PW; ++h0) {
+#pragma unroll
+      for (int t = 0; t < BK; ++t) {
+        if (nb < BK && fm[h0]) {
+          ks[nb++] = (__ffsll((long long)fm[h0]) - 1) + 64 * h0;
+          fm[h0] &= fm[h0] - 1;
+        }
+      }
+    }
+    if (nb == 0) break;
+#pragma unroll
+    for (int t = 0; t < BK; ++t)
+      if (t >= nb) ks[t] = ks[0];
+    const int LDl = pf_opaque(LD);
+    PV<PW> R[BK];
+#pragma unroll
+    for (int t = 0; t < BK; ++t)
+#pragma unroll
+      for (int h = 0; h < PW; ++h) {
+        const int j = lane + 64 * h;
+        R[t][h] = (t < nb && j < P) ? A[ks[t] * LDl + j] : 0.0;
+      }
+    // M <- the sequential sweep of B = A[K][K]: -B^-1 (identity padding)
+    double M[BK][BK];
+#pragma unroll
+    for (int t = 0; t < BK; ++t)
+#pragma unroll
+      for (int u = 0; u < BK; ++u)
+        M[t][u] = (t < nb && u < nb) ? pv_read<PW>(R[t], ks[u]) : (t == u ? -1.0 : 0.0);
+    bool ok = true;
+#pragma unroll
+    for (int p = 0; p < BK; ++p) {
+      if (p < nb) {
+        const double d = M[p][p];
+        if (!(d > 0.0)) { ok = false; break; }
+        const double inv = 1.0 / d;
+#pragma unroll
+        for (int i = 0; i < BK; ++i)
+#pragma unroll
+          for (int j = 0; j < BK; ++j)
+            if (i != p && j != p) M[i][j] = fma(-M[i][p] * inv, M[p][j], M[i][j]);
+#pragma unroll
+        for (int i = 0; i < BK; ++i)
+          if (i != p) { M[i][p] *= inv; M[p][i] = M[i][p]; }
+        M[p][p] = -inv;
+      }
+    }
+    if (!ok) {  // uniform across the workgroup
+      if (threadIdx.x == 0) sm.flag[1] = 1;
+      break;
+    }
+    // W[t][j] = (B^-1 A[K][:])[t][j] = -sum_u M[t][u] R[u][j]
+    PV<PW> W[BK];
+    bool inK[PW];
+#pragma unroll
+    for (int h = 0; h < PW; ++h) {
+      const int j = lane + 64 * h;
+      inK[h] = false;
+#pragma unroll
+      for (int t = 0; t < BK; ++t) {
+        inK[h] |= (t < nb) && (j == ks[t]);
+        double v = 0.0;
+#pragma unroll
+        for (int u = 0; u < BK; ++u) v = fma(-M[t][u], R[u][h], v);
+        W[t][h] = (t < nb) ? v : 0.0;
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < PW; ++h) {
+      const int j = lane + 64 * h;
+      if (j < P && !inK[h]) {
+        double av[RW];
+#pragma unroll
+        for (int q = 0; q < RW; ++q) {
+          const int i = min(r0 + q, P - 1);
+          av[q] = A[i * LDl + j];
+        }
+#pragma unroll
+        for (int q = 0; q < RW; ++q) {
+          const int i = r0 + q;
+          bool ik = false;
+#pragma unroll
+          for (int t = 0; t < BK; ++t) ik |= (t < nb) && (i == ks[t]);
+          if (i < P && !ik) {
+            double v = av[q];
+#pragma unroll
+            for (int t = 0; t < BK; ++t) v = fma(-pv_read<PW>(R[t], min(i, 64 * PW - 1)), W[t][h], v);
+            A[i * LDl + j] = v;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+      for (int h = 0; h < PW; ++h) {
+        const int j = lane + 64 * h;
+        if (j < P) {
+#pragma unroll
+          for (int t = 0; t < BK; ++t) {
+            if (t < nb) {
+              if (!inK[h]) {
+                A[ks[t] * LDl + j] = W[t][h];
+                A[j * LDl + ks[t]] = W[t][h];
+              } else {
+#pragma unroll
+                for (int u = 0; u < BK; ++u)
+                  if (u < nb && j == ks[u]) A[ks[t] * LDl + j] = M[t][u];
+              }
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    PF_COUNT(26);
+  }
+  __syncthreads();
+}
+
 // u = A v for the symmetric swept matrix (lane p: u_p = sum_q A[q][p] v_q;
 // v staged in LDS, read by uniform broadcast)
 template <int PW>
@@ -779,21 +932,34 @@ __device__ __forceinline__ bool polish_run(const FitKArgs &a, FitSmem<NW, KMAX, 
     if (fresh) {
       PF_STAMP(20);
       if (restored) {
+        const unsigned long long t_r0 = PF_RT();
         restore_hessian<NW, KMAX, MODE>(a, sm);
+        PF_BLKV(10, PF_RT() - t_r0);
         restore = false;
       } else {
         PF_COUNT(15);
         const bool st = a.hstash && n_newton == 0 && lam > 0.0 && lam <= lam0;
+        const unsigned long long t_h0 = PF_RT();
         hessian_collective<NW, KMAX, O0, O1, O2, MODE>(a, sm, x, gh, lam, st);
+        PF_BLKV(5, 1);
+        PF_BLKV(6, PF_RT() - t_h0);
         stashed = st;
       }
       __syncthreads();
       PF_STAMP(21);
+      const unsigned long long t_s0 = PF_RT();
+#if PF_SWEEP_BLK > 1
+      sweep_in_free_blk<NW, KMAX, MODE>(a, sm, gh, c);
+#else
       sweep_in_free<NW, KMAX, MODE>(a, sm, gh, c);
+#endif
+      PF_BLKV(7, PF_RT() - t_s0);
       PF_STAMP(24);
     }
     PF_STAMP(19);
+    const unsigned long long t_q0 = PF_RT();
     if (wave == 0) {
+      pf_serial_prio(true);
       PV<PW> z;
       int ns = 0;
       const bool ok = qp_active<NW, KMAX, MODE>(a, sm, x, gh, c, z, ns, zero, sgn_, !fresh);
@@ -811,8 +977,10 @@ __device__ __forceinline__ bool polish_run(const FitKArgs &a, FitSmem<NW, KMAX, 
       wave_sum2(dl, l1, dec, l1s);
       dec += c * l1s;
       if (lane == 0) { sm.fout[2] = ok ? dec : 0.0; sm.fout[3] = ok ? 1.0 : 0.0; }
+      pf_serial_prio(false);
     }
     __syncthreads();
+    PF_BLKV(8, PF_RT() - t_q0);
     const double dec = sm.fout[2];
     const bool qp_ok = sm.fout[3] != 0.0;
     PV<PW> d;
@@ -853,7 +1021,9 @@ __device__ __forceinline__ bool polish_run(const FitKArgs &a, FitSmem<NW, KMAX, 
     for (int ls = 0; ls < 30; ++ls) {
 #pragma unroll
       for (int h = 0; h < PW; ++h) xn[h] = x[h] + alpha * d[h];
+      const unsigned long long t_e0 = PF_RT();
       const bool bad = eval_collective<NW, KMAX, O0, O1, O2, MODE>(a, sm, xn, fn, gn);
+      PF_BLKV(9, PF_RT() - t_e0);
       ++n_eval;
       if (!bad && fn <= f + 1e-4 * alpha * dec) { acc = true; break; }
       alpha *= 0.5;

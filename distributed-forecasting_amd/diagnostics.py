@@ -167,6 +167,18 @@ def insample_metrics(engine: E.Engine, y: torch.Tensor, yhat: torch.Tensor,
     metrics the multi-GPU path all-gathers (the reference logs its CV
     metrics per series to MLflow, 02_training.py:187-192).  ``mdape=False``
     skips the median (NaN): the reference logs mse / mae / mape only."""
+    met, a = insample_args(y, yhat, yhat_lower, yhat_upper, mdape)
+    rc = engine.ctx.lib.pf_cv_metrics(engine.ctx.h, ctypes.byref(a),
+                                      ctypes.c_void_p(torch.cuda.current_stream(y.device).cuda_stream))
+    engine.ctx.check(rc, "pf_cv_metrics")
+    return met
+
+
+def insample_args(y: torch.Tensor, yhat: torch.Tensor, yhat_lower: torch.Tensor | None = None,
+                  yhat_upper: torch.Tensor | None = None, mdape: bool = True):
+    """The [n, 7] output tensor and the pf_cv_args of ``insample_metrics``
+    (also handed to pf_fit_forecast).  The tensors the args point at are
+    kept alive by both (``met._keep``, ``args._keep``)."""
     n, T = int(y.shape[0]), int(y.shape[1])
     dev = y.device
 
@@ -192,8 +204,6 @@ def insample_metrics(engine: E.Engine, y: torch.Tensor, yhat: torch.Tensor,
                    lo.data_ptr() if lo is not None else None,
                    hi.data_ptr() if hi is not None else None, met.data_ptr(), ld_y, ld_f,
                    0 if mdape else 1)
-    rc = engine.ctx.lib.pf_cv_metrics(engine.ctx.h, ctypes.byref(a),
-                                      ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
-    engine.ctx.check(rc, "pf_cv_metrics")
     met._keep = (yy, ff, lo, hi)
-    return met
+    a._keep = met._keep
+    return met, a

@@ -776,6 +776,36 @@ class Engine:
         with K4 on the current stream (both only read theta and write disjoint
         rows); the caller joins (``current.wait_stream(mc_stream)``) before
         reading the future rows' intervals."""
+        a, out, cap_s = self._predict_args(fit, fgrid, n_samples, seed, components, series_id,
+                                           interval_method, cap)
+        dev = fit.theta.device
+        if mc_stream is None:
+            a.parts = 0
+            rc = self.ctx.lib.pf_predict(self.ctx.h, ctypes.byref(a), _stream(self.device))
+            self.ctx.check(rc, "pf_predict")
+            return out
+        cur = torch.cuda.current_stream(dev)
+        mc_stream.wait_stream(cur)
+        a.parts = L.PF_PREDICT_MC
+        rc = self.ctx.lib.pf_predict(self.ctx.h, ctypes.byref(a), ctypes.c_void_p(mc_stream.cuda_stream))
+        self.ctx.check(rc, "pf_predict (mc part)")
+        if not torch.cuda.is_current_stream_capturing():
+            # everything K5 reads or writes stays allocated until it ran on the
+            # side stream (a captured graph's pool keeps its blocks anyway)
+            fgt = fgrid.tensors() if isinstance(fgrid, RaggedGrid) else \
+                [fgrid.t, fgrid.XT, fgrid.t_change, fgrid.seg]
+            extra = [t for t in (series_id, cap_s) if t is not None]
+            for v in list(out.values()) + [fit.theta, fit.y_scale] + fgt + extra:
+                v.record_stream(mc_stream)
+        a.parts = L.PF_PREDICT_DET
+        rc = self.ctx.lib.pf_predict(self.ctx.h, ctypes.byref(a), _stream(self.device))
+        self.ctx.check(rc, "pf_predict (det part)")
+        return out
+
+    def _predict_args(self, fit: FitResult, fgrid: DeviceGrid, n_samples, seed, components,
+                      series_id, interval_method, cap):
+        """pf_predict_args for ``predict`` / ``fit_forecast`` and the output
+        tensors they name.  Returns (args, out, cap_scaled or None)."""
         n = fit.theta.shape[0]
         dev = fit.theta.device
         if fit.theta.shape[1] != 3 + fgrid.S + fgrid.K:
@@ -841,25 +871,67 @@ class Engine:
             a.n_grids = fgrid.n_grids
             a.grids = fgrid.table.data_ptr()
             a.grid_of = fgrid.grid_of.data_ptr()
-        if mc_stream is None:
-            a.parts = 0
-            rc = self.ctx.lib.pf_predict(self.ctx.h, ctypes.byref(a), _stream(self.device))
-            self.ctx.check(rc, "pf_predict")
-            return out
-        cur = torch.cuda.current_stream(dev)
-        mc_stream.wait_stream(cur)
-        a.parts = L.PF_PREDICT_MC
-        rc = self.ctx.lib.pf_predict(self.ctx.h, ctypes.byref(a), ctypes.c_void_p(mc_stream.cuda_stream))
-        self.ctx.check(rc, "pf_predict (mc part)")
-        if not torch.cuda.is_current_stream_capturing():
-            # everything K5 reads or writes stays allocated until it ran on the
-            # side stream (a captured graph's pool keeps its blocks anyway)
-            fgt = fgrid.tensors() if isinstance(fgrid, RaggedGrid) else \
-                [fgrid.t, fgrid.XT, fgrid.t_change, fgrid.seg]
-            extra = [t for t in (series_id, cap_s) if t is not None]
-            for v in list(out.values()) + [fit.theta, fit.y_scale] + fgt + extra:
-                v.record_stream(mc_stream)
-        a.parts = L.PF_PREDICT_DET
-        rc = self.ctx.lib.pf_predict(self.ctx.h, ctypes.byref(a), _stream(self.device))
-        self.ctx.check(rc, "pf_predict (det part)")
-        return out
+        a._keep = (sig, s_a, s_m, fgrid)
+        return a, out, cap_s
+
+    def fit_forecast(self, grid: DeviceGrid, Y: torch.Tensor, fgrid: DeviceGrid, *,
+                     n_samples: int | None = None, seed: int = 0, components: bool = True,
+                     series_id: torch.Tensor | None = None, interval_method: str | None = None,
+                     metrics: bool | str = False, only_fused: bool = False, **opt):
+        """``fit`` + ``predict`` on ``fgrid`` (+ with ``metrics`` the in-sample
+        metrics of ``diagnostics.insample_metrics`` over the history rows;
+        "fast" skips the MDAPE median) through pf_fit_forecast: one launch
+        where the layout allows, each series' forecast and metrics computed in
+        its fit workgroup as soon as its own fit ends (the same bits as the
+        separate launches).  ``fgrid`` must carry the fit grid's changepoints
+        (``predict_grid`` / ``build_grid(t_change=grid.t_change)``).
+        Returns (FitResult, forecast dict, metrics [n, 7] or None, fused);
+        with ``only_fused`` nothing is launched unless fused (then
+        (None, None, None, False))."""
+        if isinstance(grid, RaggedGrid) or self.config.growth == "logistic":
+            if only_fused:
+                return None, None, None, False
+            fit = self.fit(grid, Y, **opt)
+            out = self.predict(fit, fgrid, n_samples=n_samples, seed=seed, components=components,
+                               series_id=series_id, interval_method=interval_method)
+            met = None
+            if metrics:
+                from .diagnostics import insample_metrics
+                met = insample_metrics(self, Y[:, :grid.T], out["yhat"], out["yhat_lower"],
+                                       out["yhat_upper"], mdape=metrics != "fast")
+            return fit, out, met, False
+        mode = self.config.fit_mode
+        polish = opt.pop("polish", None)
+        stan_faithful = opt.pop("stan_faithful", None)
+        if polish is None:
+            polish = mode != "stan"
+        if stan_faithful is None:
+            stan_faithful = mode == "stan_map"
+        n = Y.shape[0]
+        y_scale, y_scaled, theta, status, _ = self.prepare(grid, Y)
+        dev = Y.device
+        f = torch.empty(n, dtype=torch.float64, device=dev)
+        f_stan = torch.empty(n, dtype=torch.float64, device=dev)
+        n_iter = torch.empty(n, dtype=torch.int32, device=dev)
+        n_eval = torch.empty(n, dtype=torch.int32, device=dev)
+        fit = FitResult(grid, theta, y_scale, f, f_stan, status, n_iter, n_eval, self.config)
+        pb = self.problem(grid, y_scaled, n)
+        o = self.fit_opts(polish, stan_faithful, **opt)
+        a, out, _ = self._predict_args(fit, fgrid, n_samples, seed, components, series_id,
+                                       interval_method, None)
+        a.parts = 0
+        met, cva = None, None
+        if metrics:
+            from .diagnostics import insample_args
+            met, cva = insample_args(Y[:, :grid.T], out["yhat"], out["yhat_lower"],
+                                     out["yhat_upper"], mdape=metrics != "fast")
+        fused = ctypes.c_int32(0)
+        rc = self.ctx.lib.pf_fit_forecast(
+            self.ctx.h, ctypes.byref(pb), ctypes.byref(o), _ptr(theta), _ptr(f), _ptr(f_stan),
+            _ptr(status), _ptr(n_iter), _ptr(n_eval), ctypes.byref(a),
+            ctypes.byref(cva) if cva is not None else None,
+            L.PF_FF_ONLY_FUSED if only_fused else 0, ctypes.byref(fused), _stream(self.device))
+        self.ctx.check(rc, "pf_fit_forecast")
+        if only_fused and not fused.value:
+            return None, None, None, False
+        return fit, out, met, bool(fused.value)

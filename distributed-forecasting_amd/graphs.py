@@ -21,6 +21,12 @@ it: ``close()`` (or garbage collection of the step) drops the graph first and
 then destroys that context (pf_ctx_destroy).  RCCL collectives stay outside
 the graph (run them after replay).
 
+``fuse`` (default): exact intervals on one grid run fit, forecast and
+metrics as ONE launch (pf_fit_forecast, ``fused`` says whether the last step
+did): each series' forecast rows and metrics are computed in its fit
+workgroup as soon as its own fit ends — the same bits as the separate
+launches, which run otherwise (K5 on a side stream, concurrent with K4 / K6).
+
 ``metrics``: True (default) computes the whole in-sample set K6 offers
 (mse, rmse, mae, mape, smape, coverage and the MDAPE median); "fast" skips
 the MDAPE median (NaN) — the set the reference logs (mse / mae / mape,
@@ -45,7 +51,7 @@ class ForecastStep:
     def __init__(self, engine: E.Engine, ds_ns: np.ndarray, n: int, *, horizon: int = 90,
                  freq_ns: int = E.NS_PER_DAY, series_id: torch.Tensor | None = None,
                  seed: int = 0, metrics: bool | str = True, interval_method: str | None = None,
-                 components: bool = False):
+                 components: bool = False, fuse: bool = True):
         if metrics not in (True, False, "fast", "all"):
             raise ValueError("metrics must be True, False or 'fast'")
         self._owns_engine = False
@@ -67,6 +73,8 @@ class ForecastStep:
         self.metrics = metrics
         self.interval_method = interval_method
         self.components = components
+        self.fuse = fuse
+        self.fused = None     # whether the last step ran as one launch (pf_fit_forecast)
         self.graph = None
         self.out = None
         # K5 (Monte-Carlo rows) on a side stream, concurrent with K4 and K6
@@ -83,22 +91,32 @@ class ForecastStep:
                             t_scale_ns=int(self.ds[-1] - self.ds[0]),
                             n_changepoints=eng.config.n_changepoints,
                             changepoint_range=eng.config.changepoint_range, device=eng.device)
-        # the forecast grid needs only the fit grid's changepoints: build it
-        # on the side stream while the fit runs
+        # the forecast grid needs only the fit grid's changepoints
         cur = torch.cuda.current_stream(self.Y.device)
-        self.mc_stream.wait_stream(cur)
-        with torch.cuda.stream(self.mc_stream):
-            fg = E.build_grid(self.fut, self.seasons, start_ns=grid.start_ns,
-                              t_scale_ns=grid.t_scale_ns,
-                              changepoint_range=eng.config.changepoint_range,
-                              t_change=grid.t_change, device=eng.device)
+        fg = E.build_grid(self.fut, self.seasons, start_ns=grid.start_ns,
+                          t_scale_ns=grid.t_scale_ns,
+                          changepoint_range=eng.config.changepoint_range,
+                          t_change=grid.t_change, device=eng.device)
+        method = self.interval_method or eng.config.interval_method
+        if self.fuse and method == "exact":
+            # one launch: each series' forecast rows and metrics run in its fit
+            # workgroup as soon as its own fit ends (pf_fit_forecast)
+            fit, out, met, fused = eng.fit_forecast(
+                grid, self.Y, fg, seed=self.seed, components=self.components,
+                series_id=self.series_id, interval_method=self.interval_method,
+                metrics=self.metrics, only_fused=True)
+            self.fused = fused
+            if fused:
+                res = {"fit": fit, "forecast": out, "grid": grid, "forecast_grid": fg}
+                if self.metrics:
+                    res["metrics"] = met
+                return res
+        self.fused = False
         fit = eng.fit(grid, self.Y)
-        cur.wait_stream(self.mc_stream)
         out = eng.predict(fit, fg, seed=self.seed, components=self.components,
                           series_id=self.series_id, interval_method=self.interval_method,
                           mc_stream=self.mc_stream)
         res = {"fit": fit, "forecast": out, "grid": grid, "forecast_grid": fg}
-        method = self.interval_method or eng.config.interval_method
         if method == "sample":
             cur.wait_stream(self.mc_stream)     # K5 writes the history rows' intervals too
         if self.metrics:

@@ -337,6 +337,26 @@ typedef struct {
 } pf_cv_args;
 int pf_cv_metrics(pf_ctx *ctx, const pf_cv_args *args, void *stream);
 
+/* ------------------------------------ K3+K4+K5+K6: fit, forecast, metrics
+ * The results of pf_fit, then pf_predict(pred), then (cv != NULL)
+ * pf_cv_metrics(cv) on one stream — the training stage of
+ * 02_training.py:150-205 for a batch — with pred->theta == theta_inout and
+ * every part covering the pb->n_series fitted series.  Where the layout
+ * allows (one grid, PF_INTERVAL_EXACT, every forecast part, in-sample metrics
+ * (cv: n_groups = 1, window = n_rows), the warm-up hand-off fit path) it is
+ * ONE launch: each series' forecast rows and metrics run in its fit
+ * workgroup as soon as its own fit ends (bitwise the separate launches'
+ * outputs); *fused (may be NULL) says whether it was.  flags
+ * PF_FF_ONLY_FUSED: launch nothing unless fused (*fused = 0: the caller runs
+ * the parts itself, e.g. on two streams).  The metrics' y / yhat rows are
+ * read after this series' forecast rows are written (yhat = pred->yhat).   */
+enum { PF_FF_ONLY_FUSED = 1 };
+int pf_fit_forecast(pf_ctx *ctx, const pf_problem *pb, const pf_fit_opts *opts,
+                    double *theta_inout, double *f_out, double *f_stan,
+                    int32_t *status, int32_t *n_iter, int32_t *n_eval,
+                    const pf_predict_args *pred, const pf_cv_args *cv, int flags,
+                    int32_t *fused, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -145,3 +145,83 @@ def test_close_releases_the_private_context():
     assert own.ctx.closed
     with pytest.raises(RuntimeError, match="shared"):
         eng.ctx.close()
+
+
+def _cols_bits(t, T):
+    t = t[..., :T].contiguous()
+    if t.dtype == torch.float32:
+        return t.view(torch.int32)
+    if t.dtype == torch.float64:
+        return t.view(torch.int64)
+    return t
+
+
+@pytest.mark.parametrize("components,metrics", [(False, "fast"), (False, True), (True, True)])
+def test_fused_step_equals_separate_launches(components, metrics):
+    """pf_fit_forecast's one launch (fit + K4 + K5 + K6 per workgroup) gives
+    the bits of the separate fit / predict / metrics launches, eager and
+    replayed, with and without the trend bands and components."""
+    ds = synthetic.daily_dates()
+    n = 40
+    Y = synthetic.sales_matrix(n, ds, config_index=1)
+    keys = np.stack([np.ones(n, np.int64), np.arange(1, n + 1)], 1)
+    sid = torch.from_numpy(B.series_id(keys)).cuda()
+    eng = dfa.Engine(0)
+    snaps = {}
+    for fuse in (True, False):
+        st = dfa.ForecastStep(eng, ds, n, series_id=sid, components=components, metrics=metrics,
+                              fuse=fuse)
+        st.set_inputs(Y)
+        r = st.run()
+        torch.cuda.synchronize()
+        assert st.fused is fuse
+        Tf = st.Tf
+        snap = {k: _cols_bits(v, Tf).clone() for k, v in r["forecast"].items()}
+        snap.update(theta=_cols_bits(r["fit"].theta, 10 ** 6).clone(),
+                    f=_cols_bits(r["fit"].f, 10 ** 6).clone(), status=r["fit"].status.clone(),
+                    metrics=_cols_bits(r["metrics"], 10 ** 6).clone())
+        snaps[fuse] = snap
+        if fuse:
+            st.capture()
+            st.set_inputs(Y)
+            r2 = st.replay()
+            torch.cuda.synchronize()
+            for k, v in r2["forecast"].items():
+                assert torch.equal(_cols_bits(v, Tf), snap[k]), ("replay", k)
+            assert torch.equal(_cols_bits(r2["metrics"], 10 ** 6), snap["metrics"])
+        st.close()
+    a, b = snaps[True], snaps[False]
+    assert set(a) == set(b)
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+    assert (a["status"] == 70).all()
+
+
+def test_fit_forecast_falls_back_and_reports():
+    """Engine.fit_forecast: the fused call reports fused=True at a small
+    batch; with only_fused on a layout it cannot fuse (sample intervals) it
+    launches nothing; without only_fused it runs the parts."""
+    ds = synthetic.daily_dates()
+    n = 8
+    Y = synthetic.sales_matrix(n, ds, config_index=1)
+    eng = dfa.Engine(0)
+    seasons = eng.config.seasons(int(ds[0]), int(ds[-1]), int(ds[1] - ds[0]))
+    g = dfa.build_grid(ds, seasons, start_ns=int(ds[0]), t_scale_ns=int(ds[-1] - ds[0]))
+    Yd = torch.zeros((n, g.T_pad), dtype=torch.float64, device="cuda")
+    Yd[:, :g.T] = torch.from_numpy(Y).cuda()
+    fg = dfa.build_grid(dfa.future_dates(ds, 90), seasons, start_ns=g.start_ns,
+                        t_scale_ns=g.t_scale_ns, t_change=g.t_change)
+    fit, out, met, fused = eng.fit_forecast(g, Yd, fg, components=False, metrics="fast")
+    assert fused and met is not None and out["yhat"].shape[0] == n
+    ref = eng.fit(g, Yd)
+    o2 = eng.predict(ref, fg, components=False)
+    torch.cuda.synchronize()
+    T = fg.T
+    assert torch.equal(_cols_bits(out["yhat_lower"], T), _cols_bits(o2["yhat_lower"], T))
+    r = eng.fit_forecast(g, Yd, fg, interval_method="sample", only_fused=True)
+    assert r == (None, None, None, False)
+    fit3, out3, met3, fused3 = eng.fit_forecast(g, Yd, fg, interval_method="sample",
+                                                components=False, metrics=True)
+    torch.cuda.synchronize()
+    assert not fused3 and met3 is not None
+    assert torch.equal(_cols_bits(out3["yhat"], T), _cols_bits(o2["yhat"], T))
