@@ -407,97 +407,118 @@ __device__ __forceinline__ void mc_rows(const PredKArgs &a, const PredSeries &ps
     const float lf_capy = (float)(ysc * capr);
     float o_ylo = 0.f, o_yhi = 0.f, o_tlo = 0.f, o_thi = 0.f;
     PF_STAMP1(2);
-    for (int r = 0; r < nr; ++r) {
-      PF_STAMP1(3);
-      if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) PF_COUNT(9);
+    // the samples of row c0 + r: v (yhat) and, with TR, tv (trend); advances
+    // the per-sample changepoint state to the row's time
+    auto gen_row = [&](int r, float (&v)[PF_NQ], float (&tv)[TR ? PF_NQ : 1]) {
       const int row = c0 + r;
       const float tau = readlane_f32(lf_tau, r);
       const float trendf = readlane_f32(lf_trend, r);
       const float u1 = readlane_f32(lf_u1, r), addf = readlane_f32(lf_add, r);
-      // v: the yhat samples; tv: the trend samples (kept only for trend bands)
-      float v[PF_NQ], tv[TR ? PF_NQ : 1];
-      float ylo, yhi, tlo = trendf, thi = trendf;
       float z[PF_NQ];
-      {
-        const float capy = readlane_f32(lf_capy, r);
-        if constexpr (DIRECT) {
-          mc_row_normals(a, sid, row, z);
+      const float capy = readlane_f32(lf_capy, r);
+      if constexpr (DIRECT) {
+        mc_row_normals(a, sid, row, z);
+#pragma unroll
+        for (int q = 0; q < PF_NQ; ++q) {
+          const int smp = lane + 64 * q;
+          const float ts = (smp < N) ? mc_trend_direct(a.seed0, a.seed1, sid, smp, (int)s_meta[smp], t_max, lam,
+                                                       (double)tau, logi, (double)trendf, ysc, (double)capy, k0, m0)
+                                     : __builtin_nanf("");
+          if constexpr (TR) tv[q] = ts;
+          v[q] = (smp < N) ? fmaf(sd, z[q], fmaf(ts, u1, addf)) : __builtin_nanf("");
+        }
+      } else {
+        // absorb the changepoints passed since the previous row: one pass
+        // over the samples with the next changepoint held in registers (the
+        // LDS loads of different samples overlap), repeated only if a sample
+        // passed two changepoints since the previous row
+        while (true) {
 #pragma unroll
           for (int q = 0; q < PF_NQ; ++q) {
-            const int smp = lane + 64 * q;
-            const float ts = (smp < N) ? mc_trend_direct(a.seed0, a.seed1, sid, smp, (int)s_meta[smp], t_max, lam,
-                                                         (double)tau, logi, (double)trendf, ysc, (double)capy, k0, m0)
-                                       : __builtin_nanf("");
-            if constexpr (TR) tv[q] = ts;
-            v[q] = (smp < N) ? fmaf(sd, z[q], fmaf(ts, u1, addf)) : __builtin_nanf("");
-          }
-        } else {
-          // absorb the changepoints passed since the previous row: one pass
-          // over the samples with the next changepoint held in registers (the
-          // LDS loads of different samples overlap), repeated only if a sample
-          // passed two changepoints since the previous row
-          while (true) {
-#pragma unroll
-            for (int q = 0; q < PF_NQ; ++q) {
-              const bool cr = tau >= nxt[q];
-              if (__ballot(cr) != 0ull) {
-                if (cr) {
-                  const uint32_t p = (st[q] & 0x1FFFu) + 1u, e = (st[q] >> 13) & 0x1FFFu;
-                  if (!logi) {
-                    s1[q] += nxd[q];
-                    s2[q] = fmaf(nxd[q], nxt[q], s2[q]);
-                  } else {
-                    const float kn = s1[q] + nxd[q];
-                    s2[q] = s2[q] + (1.0f + nxt[q] - s2[q]) * (1.0f - s1[q] / kn);
-                    s1[q] = kn;
-                  }
-                  st[q] = (st[q] & ~0x1FFFu) | p | PF_MC_ABS;
-                  const float2 cp = (p < e) ? s_cp[p] : make_float2(INFINITY, 0.0f);
-                  nxt[q] = cp.x;
-                  nxd[q] = cp.y;
+            const bool cr = tau >= nxt[q];
+            if (__ballot(cr) != 0ull) {
+              if (cr) {
+                const uint32_t p = (st[q] & 0x1FFFu) + 1u, e = (st[q] >> 13) & 0x1FFFu;
+                if (!logi) {
+                  s1[q] += nxd[q];
+                  s2[q] = fmaf(nxd[q], nxt[q], s2[q]);
+                } else {
+                  const float kn = s1[q] + nxd[q];
+                  s2[q] = s2[q] + (1.0f + nxt[q] - s2[q]) * (1.0f - s1[q] / kn);
+                  s1[q] = kn;
                 }
+                st[q] = (st[q] & ~0x1FFFu) | p | PF_MC_ABS;
+                const float2 cp = (p < e) ? s_cp[p] : make_float2(INFINITY, 0.0f);
+                nxt[q] = cp.x;
+                nxd[q] = cp.y;
               }
             }
-            unsigned long long more = 0ull;
-#pragma unroll
-            for (int q = 0; q < PF_NQ; ++q) more |= __ballot(tau >= nxt[q]);
-            if (more == 0ull) break;
           }
-          PF_STAMP1(4);
-          mc_row_normals(a, sid, row, z);
-          PF_STAMP1(5);
-          const float ysf = (float)ysc;
+          unsigned long long more = 0ull;
 #pragma unroll
-          for (int q = 0; q < PF_NQ; ++q) {
-            float trs_s;
-            if (!logi) trs_s = fmaf(ysf, fmaf(s1[q], tau, -s2[q]), trendf);
-            else trs_s = (st[q] & PF_MC_ABS) ? capy / (1.0f + __expf(-(s1[q] * (1.0f + tau - s2[q])))) : trendf;
-            const bool on = lane + 64 * q < N;
-            if constexpr (TR) tv[q] = on ? trs_s : __builtin_nanf("");
-            v[q] = on ? fmaf(sd, z[q], fmaf(trs_s, u1, addf)) : __builtin_nanf("");
-          }
+          for (int q = 0; q < PF_NQ; ++q) more |= __ballot(tau >= nxt[q]);
+          if (more == 0ull) break;
+        }
+        PF_STAMP1(4);
+        mc_row_normals(a, sid, row, z);
+        PF_STAMP1(5);
+        const float ysf = (float)ysc;
+#pragma unroll
+        for (int q = 0; q < PF_NQ; ++q) {
+          float trs_s;
+          if (!logi) trs_s = fmaf(ysf, fmaf(s1[q], tau, -s2[q]), trendf);
+          else trs_s = (st[q] & PF_MC_ABS) ? capy / (1.0f + __expf(-(s1[q] * (1.0f + tau - s2[q])))) : trendf;
+          const bool on = lane + 64 * q < N;
+          if constexpr (TR) tv[q] = on ? trs_s : __builtin_nanf("");
+          v[q] = on ? fmaf(sd, z[q], fmaf(trs_s, u1, addf)) : __builtin_nanf("");
         }
       }
-      PF_STAMP1(6);
-      if constexpr (TR) {
+    };
+    if constexpr (TR) {
+      for (int r = 0; r < nr; ++r) {
+        PF_STAMP1(3);
+        if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) PF_COUNT(9);
+        float v[PF_NQ], tv[PF_NQ];
+        gen_row(r, v, tv);
+        PF_STAMP1(6);
         float o0[4], o1[4];
         // (the trend sets are tie-heavy: the moment threshold rarely fits them)
         wave_tail_select<4>(v, tv, kk4, buf, o0, o1);
         if (N == 1) { for (int s = 0; s < 4; ++s) o1[s] = o0[s]; }
-        ylo = np_lerp(o0[0], o1[0], a.fr_lo);
-        yhi = np_lerp(-o1[1], -o0[1], a.fr_hi);
-        tlo = np_lerp(o0[2], o1[2], a.fr_lo);
-        thi = np_lerp(-o1[3], -o0[3], a.fr_hi);
-      } else {
-        // yhat tails only (no trend bands requested)
-        float o0[2], o1[2];
-        wave_tail_select<2>(v, v, kk2, buf, o0, o1, a.zthr, N);
-        if (N == 1) { o1[0] = o0[0]; o1[1] = o0[1]; }
-        ylo = np_lerp(o0[0], o1[0], a.fr_lo);
-        yhi = np_lerp(-o1[1], -o0[1], a.fr_hi);
+        const float ylo = np_lerp(o0[0], o1[0], a.fr_lo);
+        const float yhi = np_lerp(-o1[1], -o0[1], a.fr_hi);
+        const float tlo = np_lerp(o0[2], o1[2], a.fr_lo);
+        const float thi = np_lerp(-o1[3], -o0[3], a.fr_hi);
+        PF_STAMP1(7);
+        if (lane == r) { o_ylo = ylo; o_yhi = yhi; o_tlo = tlo; o_thi = thi; }
       }
-      PF_STAMP1(7);
-      if (lane == r) { o_ylo = ylo; o_yhi = yhi; o_tlo = tlo; o_thi = thi; }
+    } else {
+      // yhat tails only (no trend bands requested): two rows per selection
+      // (four interleaved key sets: more independent work per step)
+      for (int r = 0; r < nr; r += 2) {
+        PF_STAMP1(3);
+        if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) PF_COUNT(9);
+        float v0[PF_NQ], v1[PF_NQ], unused[1];
+        gen_row(r, v0, unused);
+        const bool two = r + 1 < nr;
+        if (two) gen_row(r + 1, v1, unused);
+        PF_STAMP1(6);
+        if (two) {
+          float o0[4], o1[4];
+          wave_tail_select<4>(v0, v1, kk4, buf, o0, o1, a.zthr, N);
+          if (N == 1) { for (int s = 0; s < 4; ++s) o1[s] = o0[s]; }
+          const float ylo0 = np_lerp(o0[0], o1[0], a.fr_lo), yhi0 = np_lerp(-o1[1], -o0[1], a.fr_hi);
+          const float ylo1 = np_lerp(o0[2], o1[2], a.fr_lo), yhi1 = np_lerp(-o1[3], -o0[3], a.fr_hi);
+          if (lane == r) { o_ylo = ylo0; o_yhi = yhi0; }
+          if (lane == r + 1) { o_ylo = ylo1; o_yhi = yhi1; }
+        } else {
+          float o0[2], o1[2];
+          wave_tail_select<2>(v0, v0, kk2, buf, o0, o1, a.zthr, N);
+          if (N == 1) { o1[0] = o0[0]; o1[1] = o0[1]; }
+          if (lane == r) { o_ylo = np_lerp(o0[0], o1[0], a.fr_lo); o_yhi = np_lerp(-o1[1], -o0[1], a.fr_hi); }
+        }
+        PF_STAMP1(7);
+      }
     }
     if (rv) {
       const size_t o = (size_t)series * a.Tp + myrow;

@@ -4,7 +4,8 @@
 
 Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --kernel-trace --stats of
 bench.py), profiles/<tag>_pmc.json (per-kernel averages of every counter) and
-profiles/pmc_k_fit.json (the k_fit HBM bytes per launch bench.py reports as
+profiles/pmc_k_fit.json (the HBM bytes per launch of the headline's dominant
+kernel — k_fit_forecast, else k_fit_polish — bench.py reports as
 roofline.traffic).  HBM bytes = 2*FETCH_SIZE + WRITE_SIZE (KiB -> bytes): on
 gfx950 FETCH_SIZE counts half of a wide coalesced read stream
 (MI355X_MICROARCH.md §HBM)."""
@@ -65,7 +66,7 @@ def main(src, tag):
             d["mfma_busy_per_cu_busy"] = d["SQ_VALU_MFMA_BUSY_CYCLES"] / d["SQ_BUSY_CU_CYCLES"]
     with open(os.path.join(prof, f"{tag}_pmc.json"), "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
-    kf = "k_fit_polish" if "k_fit_polish" in out else "k_fit"
+    kf = next((k for k in ("k_fit_forecast", "k_fit_polish", "k_fit") if k in out), "k_fit")
     if keep_fit and kf in out and "hbm_bytes_per_launch" in out[kf]:
         with open(os.path.join(prof, "pmc_k_fit.json"), "w") as f:
             json.dump({"tag": tag, "kernel": kf,
@@ -82,7 +83,8 @@ def main(src, tag):
             json.dump({"tag": tag, "kernel": "k_predict_mc", "n_series": 500, "horizon": 90,
                        "SQ_INSTS_VALU": d["SQ_INSTS_VALU"], "avg_ns": d.get("avg_ns"),
                        "SQ_WAVES": d.get("SQ_WAVES")}, f, indent=1)
-    for k in ("k_fit", "k_fit_polish", "k_fit_tile", "k_polish", "k_predict_det", "k_predict_mc"):
+    for k in ("k_fit", "k_fit_polish", "k_fit_forecast", "k_fit_tile", "k_polish", "k_predict_det",
+              "k_predict_mc"):
         if k in out:
             print(k, {a: (round(b, 4) if isinstance(b, float) else b) for a, b in out[k].items()})
 
