@@ -322,19 +322,20 @@ def main():
             k[1] += 1
         return {k: v[0] / v[1] for k, v in kern.items()}
 
-    def timed(fn, steps, warm=1, ctx=None, drain=None):
+    def timed(fn, steps, warm=1, ctx=None, drain=None, kernels=True):
         """Same bracketing as the headline: warm-up, barrier + sync, `steps`
         calls, barrier + sync, max over ranks; kernel averages from the HIP
-        events of the engine context the launches go through.  ``drain``
-        completes work still in flight (asynchronous exchanges) inside the
-        timed region."""
+        events of the engine context the launches go through (``kernels``:
+        off for the host-bound drop-in legs, whose launches would each pay
+        two event records).  ``drain`` completes work still in flight
+        (asynchronous exchanges) inside the timed region."""
         ctx = ctx or eng.ctx
         for _ in range(warm):
             fn()
         if drain:
             drain()
         bracket()
-        ctx.set_timing(True)
+        ctx.set_timing(kernels)
         t0_ = time.perf_counter()
         r = None
         for _ in range(steps):
@@ -656,7 +657,7 @@ def dropin(args, eng, keys, ds, Y, Yd, rank, world, bracket, max_over_ranks, sum
                 g = parallel.gather_results(kt, None, mt)
                 met = g["metrics"]
         return fr, met
-    el, ka, (fr, _) = timed(fsi, steps, warm=2)
+    el, ka, (fr, _) = timed(fsi, steps, warm=3, kernels=False)
     out["forecast_store_items"] = {
         "value": tot * steps / el, "unit": "series/s", "ms_per_call": el / steps * 1e3,
         "rows_out": int(len(fr)),
@@ -685,7 +686,7 @@ def dropin(args, eng, keys, ds, Y, Yd, rank, world, bracket, max_over_ranks, sum
         inp = pd.DataFrame({"ds": np.tile(futd.astype("datetime64[ns]"), n),
                             "store": np.repeat(keys[:, 0], len(futd)).astype(np.int32),
                             "item": np.repeat(keys[:, 1], len(futd)).astype(np.int32)})
-        el, ka, _ = timed(lambda: model.predict(None, inp), steps, warm=2)
+        el, ka, _ = timed(lambda: model.predict(None, inp), steps, warm=3, kernels=False)
         out["pyfunc_predict"] = {
             "value": tot * steps / el, "unit": "series/s", "ms_per_call": el / steps * 1e3,
             "note": "ForecastStoreItemModel.predict(context, model_input) (model_wrapper.py:43-73) "

@@ -297,6 +297,46 @@ class FittedBatch:
         hd = fit_ds if history_dates is None else history_dates
         return cls(engine, fit, np.unique(hd), fit_ds, series_ids)
 
+    @classmethod
+    def fit_forecast_dense(cls, engine: E.Engine, fit_ds: np.ndarray, Y, future_ds: np.ndarray, *,
+                           history_dates=None, series_ids=None, seed: int = 0,
+                           components: bool = False):
+        """``fit_dense`` followed by ``predict(future_ds)`` through
+        Engine.fit_forecast: one launch where the layout allows (each series'
+        forecast rows run in its fit workgroup as soon as its fit ends), the
+        same bits as the two calls.  Returns (batch, T, forecast dict)."""
+        cfg = engine.config
+        fit_ds = np.asarray(fit_ds, np.int64)
+        T = fit_ds.shape[0]
+        if T < 2:
+            raise ValueError("Dataframe has less than 2 non-NaN rows.")
+        start, t_scale = int(fit_ds[0]), int(fit_ds[-1] - fit_ds[0])
+        if t_scale <= 0:
+            raise ValueError("history must span more than one distinct date")
+        seasons = cfg.seasons(start, int(fit_ds[-1]), min_positive_diff(fit_ds))
+        grid = E.build_grid(fit_ds, seasons, start_ns=start, t_scale_ns=t_scale,
+                            n_changepoints=cfg.n_changepoints,
+                            changepoint_range=cfg.changepoint_range, device=engine.device)
+        future_ds = np.asarray(future_ds, np.int64)
+        fg = E.build_grid(future_ds, seasons, start_ns=start, t_scale_ns=t_scale,
+                          changepoint_range=cfg.changepoint_range, t_change=grid.t_change,
+                          device=engine.device)
+        dev = torch.device("cuda", engine.device)
+        n = int(Y.shape[0])
+        Yd = torch.zeros((n, grid.T_pad), dtype=torch.float64, device=dev)
+        if isinstance(Y, torch.Tensor):
+            Yd[:, :T] = Y[:, :T].to(dev, torch.float64)
+        else:
+            Yd[:, :T] = E._to_device_async(np.asarray(Y, dtype=np.float64), dev)
+        sid = None if series_ids is None else \
+            E._to_device_async(np.asarray(series_ids, dtype=np.int32), dev)
+        fit, out, _, _ = engine.fit_forecast(grid, Yd, fg, seed=seed, components=components,
+                                             series_id=sid)
+        hd = fit_ds if history_dates is None else history_dates
+        fb = cls(engine, fit, np.unique(hd), fit_ds, None)
+        fb.series_ids = sid
+        return fb, int(fg.T), out
+
     def spec(self) -> GridSpec:
         g = self.fit.grid
         return GridSpec(list(g.seasons), int(g.start_ns), int(g.t_scale_ns), g.t_change, g.holidays)

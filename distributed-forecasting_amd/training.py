@@ -330,12 +330,19 @@ def forecast_store_items(df: pd.DataFrame, keys=("store", "item"), *, periods: i
         if len(pack) == 1:
             bk = bks[0]
             bkeys = gkeys[bk.members]
-            Yd = B._dense(bk.Y, bk.Y.shape[0], bk.Y.shape[1], bk.Y.shape[1], dev) \
-                if cv_metrics else bk.Y
-            fb = B.FittedBatch.fit_dense(eng, bk.fit_ds, Yd, history_dates=bk.history_dates,
-                                         series_ids=B.series_id(bkeys))
             futs = [B.future_dates(bk.history_dates, periods, freq, include_history=True)]
-            Tf, out = fb.predict(futs[0], seed=seed, components=False)
+            if cv_metrics or cfg.growth == "logistic":
+                Yd = B._dense(bk.Y, bk.Y.shape[0], bk.Y.shape[1], bk.Y.shape[1], dev) \
+                    if cv_metrics else bk.Y
+                fb = B.FittedBatch.fit_dense(eng, bk.fit_ds, Yd, history_dates=bk.history_dates,
+                                             series_ids=B.series_id(bkeys))
+                Tf, out = fb.predict(futs[0], seed=seed, components=False)
+            else:
+                # fit + forecast in one launch (pf_fit_forecast)
+                Yd = bk.Y
+                fb, Tf, out = B.FittedBatch.fit_forecast_dense(
+                    eng, bk.fit_ds, bk.Y, futs[0], history_dates=bk.history_dates,
+                    series_ids=B.series_id(bkeys), seed=seed, components=False)
             blk = torch.stack([out[k][:, :Tf] for k in ("yhat", "yhat_upper", "yhat_lower")])
             row0 = [0, len(bk.members)]
             subs = [(bkeys, fb, Yd)]
