@@ -78,7 +78,7 @@ def main():
         seasons = [("yearly", 365.25, 10), ("weekly", 7.0, 3), ("daily", 1.0, 4)]
         hol = H.holiday_spec(H.synthetic_holidays([2017, 2018]), cfg.holidays_prior_scale,
                              cfg.seasonality_mode)
-        horizon, step_ns, method, chunk = 90, synthetic.NS_PER_HOUR, args.method or "exact", args.chunk or 10_000
+        horizon, step_ns, method, chunk = 90, synthetic.NS_PER_HOUR, args.method or "exact", args.chunk or 50_000
         work = (f"configs[4]: {n} hourly series x 8760 steps, logistic growth (cap = 1.2 max y), "
                 f"daily+weekly+yearly + 10 holidays/yr (K = 44, P = 72), 90-step forecast, "
                 f"1000-sample intervals")
