@@ -54,6 +54,8 @@ struct pf_ctx {
   char err[512];
   void *ws;         // scratch owned by the context (lane-blocked grid copy)
   size_t ws_bytes;
+  void *ws2;        // fused launch's work-sharing counters (pf_fit_forecast)
+  size_t ws2_bytes;
   int timing;       // record events around launches
   int n_timed;      // records since the last pf_read_timings
   int n_events;     // event pairs created so far
@@ -2296,7 +2298,17 @@ struct FuseArgs {
   PredKArgs p;
   CvKArgs cv;
   int metrics;  // run K6 (in-sample: one group of every history row)
+  // K5 work sharing: a series' random rows are PF_FF_BLOCKS row blocks; its
+  // own workgroup claims them first, workgroups whose series are done claim
+  // the rest.  ctl (zeroed per launch): [0] workgroups started, [1] blocks
+  // not yet claimed (set by the host to n * PF_FF_BLOCKS), then ready[n],
+  // claimed[n], finished[n]
+  int *ctl;
 };
+#ifndef PF_FF_BLOCKS
+#define PF_FF_BLOCKS 4
+#endif
+#define PF_FF_SPIN 4000   // a helper's bounded wait for work (x ~1 us of s_sleep)
 // what pf_fit_forecast asks of the fit launcher: fuse when the fit takes the
 // fused fit + polish path (done = 1); only = 1: launch nothing otherwise
 struct FuseReq {
@@ -2316,14 +2328,66 @@ struct FuseSmem {
   static constexpr size_t part_off = r0_off + 16;
   static constexpr size_t hist_off = part_off + PF_CV_INS_WAVES * 6 * sizeof(double);
   static constexpr size_t bad_off = hist_off + 256 * sizeof(int);
-  static constexpr size_t bytes = bad_off + 16;
+  static constexpr size_t bytes = bad_off + 32;   // K6's s_bad, then 4 broadcast slots
 };
 static_assert(PF_CV_INS_CACHE * sizeof(unsigned long long) <= PF_MC_CPCAP * sizeof(float2),
               "K6 cache must fit the changepoint slots it aliases");
 
+// The K5 setup of series t (ps holds its PredSeries): first random row and
+// every sample's changepoints packed in LDS.  Every thread calls it.
+__device__ __forceinline__ void ff_setup(const FuseArgs &e, const PredSeries &ps, int t, char *smem_raw) {
+  const PredKArgs &pa = e.p;
+  const uint32_t sid = pa.series_id ? pa.series_id[t] : (uint32_t)t;
+  int *s_r0 = reinterpret_cast<int *>(smem_raw + FuseSmem::r0_off);
+  if (threadIdx.x == 0) *s_r0 = pa.Tf;
+  __syncthreads();
+  mc_setup(pa, ps, sid, reinterpret_cast<float2 *>(smem_raw + FuseSmem::cp_off),
+           reinterpret_cast<uint32_t *>(smem_raw + FuseSmem::meta_off),
+           reinterpret_cast<double *>(smem_raw + FuseSmem::wsum_off), s_r0);
+}
+
+// Row block b of series t (after ff_setup of t), then — for the workgroup
+// that finishes the series' last block — its K6 row.  Returns true when K6
+// ran (its APE cache overwrote the packed changepoints).  Every thread calls it.
+__device__ __forceinline__ bool ff_rows(const FuseArgs &e, const PredSeries &ps, int t, int b,
+                                        char *smem_raw, int *s_bcast) {
+  const PredKArgs &pa = e.p;
+  const int n = pa.n_series;
+  int *finished = e.ctl + 2 + 2 * n;
+  const uint32_t sid = pa.series_id ? pa.series_id[t] : (uint32_t)t;
+  const float2 *s_cp = reinterpret_cast<const float2 *>(smem_raw + FuseSmem::cp_off);
+  const uint32_t *s_meta = reinterpret_cast<const uint32_t *>(smem_raw + FuseSmem::meta_off);
+  float *s_buf = reinterpret_cast<float *>(smem_raw + FuseSmem::buf_off);
+  const double *s_wsum = reinterpret_cast<const double *>(smem_raw + FuseSmem::wsum_off);
+  const int *s_r0 = reinterpret_cast<const int *>(smem_raw + FuseSmem::r0_off);
+  if (pa.tr) mc_block_rows<true>(pa, ps, t, sid, b, PF_FF_BLOCKS, s_cp, s_meta, s_buf, s_wsum, s_r0);
+  else mc_block_rows<false>(pa, ps, t, sid, b, PF_FF_BLOCKS, s_cp, s_meta, s_buf, s_wsum, s_r0);
+  __syncthreads();   // this block's rows written by every wave
+  if (threadIdx.x == 0) {
+    __threadfence();  // the rows visible device-wide before the count says so
+    s_bcast[0] = atomicAdd(&finished[t], 1);
+  }
+  __syncthreads();
+  const int done_before = s_bcast[0];
+  __syncthreads();
+  if (!(e.metrics && done_before == PF_FF_BLOCKS - 1)) return false;
+  // the series' last block: every row of t is written (its K4 rows before it
+  // was published, the other blocks before their counts)
+  __threadfence();
+  cv_insample_block(e.cv, t, reinterpret_cast<unsigned long long *>(smem_raw + FuseSmem::cache_off),
+                    reinterpret_cast<double (*)[6]>(smem_raw + FuseSmem::part_off),
+                    reinterpret_cast<int *>(smem_raw + FuseSmem::hist_off),
+                    reinterpret_cast<int *>(smem_raw + FuseSmem::bad_off));
+  __syncthreads();
+  return true;
+}
+
 template <int NW, int KMAX, int O0, int O1, int O2, int MODE>
 __global__ __launch_bounds__(NW * 64, FitOcc<KMAX>::W) void k_fit_forecast(FitKArgs a, FuseArgs e) {
   static_assert(NW == PF_MC_WAVES && NW == PF_CV_INS_WAVES, "fused epilogue: one block shape");
+  const int n = e.p.n_series;
+  int *ready = e.ctl + 2, *claimed = e.ctl + 2 + n;
+  if (threadIdx.x == 0) atomicAdd(&e.ctl[0], 1);   // started
   PF_BLK(0);
   pf_base_prio(1);
   fit_polish_passes<NW, KMAX, O0, O1, O2, MODE>(a);
@@ -2332,15 +2396,10 @@ __global__ __launch_bounds__(NW * 64, FitOcc<KMAX>::W) void k_fit_forecast(FitKA
   pf_base_prio(0);
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   PredSeries &ps = *reinterpret_cast<PredSeries *>(smem_raw);
-  float2 *s_cp = reinterpret_cast<float2 *>(smem_raw + FuseSmem::cp_off);
-  uint32_t *s_meta = reinterpret_cast<uint32_t *>(smem_raw + FuseSmem::meta_off);
-  float *s_buf = reinterpret_cast<float *>(smem_raw + FuseSmem::buf_off);
-  double *s_wsum = reinterpret_cast<double *>(smem_raw + FuseSmem::wsum_off);
-  int *s_r0 = reinterpret_cast<int *>(smem_raw + FuseSmem::r0_off);
+  int *s_bcast = reinterpret_cast<int *>(smem_raw + FuseSmem::bad_off + 8);
   const int series = blockIdx.x;
   const PredKArgs &pa = e.p;
   const uint32_t sid = pa.series_id ? pa.series_id[series] : (uint32_t)series;
-  if (threadIdx.x == 0) *s_r0 = pa.Tf;
   pred_setup(pa, series, ps);
   __syncthreads();
   // K4: every row's point forecast (+ components), the deterministic rows'
@@ -2348,21 +2407,100 @@ __global__ __launch_bounds__(NW * 64, FitOcc<KMAX>::W) void k_fit_forecast(FitKA
   const double t_max = pa.t[pa.Tf - 1];
   for (int row = threadIdx.x; row < pa.Tf; row += NW * 64)
     det_row(pa, ps, series, sid, row, t_max, e.p.comp_col0, e.p.comp_ncol);
-  // K5: the random-trend rows' Monte-Carlo intervals
-  if (pa.N > 0) {
-    if (pa.tr) mc_block<true>(pa, ps, series, sid, 0, 1, s_cp, s_meta, s_buf, s_wsum, s_r0);
-    else mc_block<false>(pa, ps, series, sid, 0, 1, s_cp, s_meta, s_buf, s_wsum, s_r0);
-  }
-  if (!e.metrics) {
-    __syncthreads();
+  if (pa.N == 0) {
+    if (e.metrics) {
+      __syncthreads();
+      cv_insample_block(e.cv, series, reinterpret_cast<unsigned long long *>(smem_raw + FuseSmem::cache_off),
+                        reinterpret_cast<double (*)[6]>(smem_raw + FuseSmem::part_off),
+                        reinterpret_cast<int *>(smem_raw + FuseSmem::hist_off),
+                        reinterpret_cast<int *>(smem_raw + FuseSmem::bad_off));
+    }
     PF_BLK(2);
     return;
   }
-  __syncthreads();   // this series' yhat / intervals written
-  cv_insample_block(e.cv, series, reinterpret_cast<unsigned long long *>(smem_raw + FuseSmem::cache_off),
-                    reinterpret_cast<double (*)[6]>(smem_raw + FuseSmem::part_off),
-                    reinterpret_cast<int *>(smem_raw + FuseSmem::hist_off),
-                    reinterpret_cast<int *>(smem_raw + FuseSmem::bad_off));
+  // publish: theta and the K4 rows of this series are final
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    atomicExch(&ready[series], 1);
+  }
+  // K5: row blocks claimed one at a time — this series' first (helpers may
+  // take some), then other published series' blocks while any are left.  A
+  // workgroup waits for work only once every workgroup of the launch has
+  // started (the series it waits on are resident, so they finish), and only
+  // for a bounded time; the owner of a series always takes its unclaimed
+  // blocks itself, so the results never depend on helping.  One call site
+  // of the block body (its registers are allocated once).
+  int cur = series;   // the series whose PredSeries is in ps
+  int cur_setup = -1; // the series whose K5 setup is in LDS
+  bool own = true;
+  int spin = 0;
+  while (true) {
+    if (threadIdx.x < 64) {
+      const int lane = pf_lane();
+      int t = -1, b = PF_FF_BLOCKS, act = 2;
+      if (own) {
+        if (lane == 0) {
+          b = atomicAdd(&claimed[series], 1);
+          if (b < PF_FF_BLOCKS) atomicSub(&e.ctl[1], 1);
+        }
+        b = __shfl(b, 0, 64);
+        t = series;
+        act = b < PF_FF_BLOCKS ? 0 : 3;   // 3: own blocks done, look for others
+      } else {
+        // wave 0 scans for an unclaimed block of a published series,
+        // starting after its own index
+        for (int base = 0; base < n && t < 0; base += 64) {
+          const int u = (series + 1 + base + lane) % n;
+          const bool cand = (base + lane < n - 1) &&
+                            __atomic_load_n(&ready[u], __ATOMIC_RELAXED) != 0 &&
+                            __atomic_load_n(&claimed[u], __ATOMIC_RELAXED) < PF_FF_BLOCKS;
+          const unsigned long long m = __ballot(cand);
+          if (m) t = __shfl(u, __ffsll((long long)m) - 1, 64);
+        }
+        if (lane == 0) {
+          if (t >= 0) {
+            b = atomicAdd(&claimed[t], 1);
+            if (b < PF_FF_BLOCKS) atomicSub(&e.ctl[1], 1);
+          }
+          const int left = __atomic_load_n(&e.ctl[1], __ATOMIC_RELAXED);
+          const int started = __atomic_load_n(&e.ctl[0], __ATOMIC_RELAXED);
+          act = (t >= 0 && b < PF_FF_BLOCKS) ? 0 : 1;   // 0: work; 1: wait; 2: exit
+          if (act == 1 && (left <= 0 || started < n || spin >= PF_FF_SPIN)) act = 2;
+        }
+      }
+      if (lane == 0) {
+        s_bcast[1] = act;
+        s_bcast[2] = t;
+        s_bcast[3] = b;
+      }
+    }
+    __syncthreads();
+    const int act = s_bcast[1], tt = s_bcast[2], bb = s_bcast[3];
+    __syncthreads();
+    if (act == 2) break;
+    if (act == 3) {
+      own = false;
+      continue;
+    }
+    if (act == 1) {
+      ++spin;
+      __builtin_amdgcn_s_sleep(127);
+      continue;
+    }
+    spin = 0;
+    if (tt != cur) {
+      __threadfence();   // acquire: the series' theta and K4 rows
+      pred_setup(pa, tt, ps);
+      cur = tt;
+      __syncthreads();
+    }
+    if (tt != cur_setup) {
+      ff_setup(e, ps, tt, smem_raw);
+      cur_setup = tt;
+    }
+    if (ff_rows(e, ps, tt, bb, smem_raw, s_bcast)) cur_setup = -1;
+  }
   PF_BLK(2);
 }
 
@@ -2378,6 +2516,8 @@ int pf_ctx_create(int device, pf_ctx **out) {
   c->device = device;
   c->err[0] = 0;
   c->ws = nullptr;
+  c->ws2 = nullptr;
+  c->ws2_bytes = 0;
   c->ws_bytes = 0;
   c->timing = 0;
   c->n_timed = 0;
@@ -2423,6 +2563,7 @@ int pf_ctx_destroy(pf_ctx *ctx) {
       (void)hipEventDestroy(ctx->timed[i].stop);
     }
   if (ctx && ctx->ws) (void)hipFree(ctx->ws);
+  if (ctx && ctx->ws2) (void)hipFree(ctx->ws2);
   delete ctx;
   return 0;
 }
@@ -2438,6 +2579,18 @@ static int ctx_workspace(pf_ctx *ctx, size_t bytes, void **out) {
     ctx->ws_bytes = bytes;
   }
   *out = ctx->ws;
+  return 0;
+}
+
+static int ctx_workspace2(pf_ctx *ctx, size_t bytes, void **out) {
+  if (bytes > ctx->ws2_bytes) {
+    if (ctx->ws2) PF_HIP(ctx, hipFree(ctx->ws2));
+    ctx->ws2 = nullptr;
+    ctx->ws2_bytes = 0;
+    PF_HIP(ctx, hipMalloc(&ctx->ws2, bytes));
+    ctx->ws2_bytes = bytes;
+  }
+  *out = ctx->ws2;
   return 0;
 }
 
@@ -3313,6 +3466,17 @@ int pf_fit_forecast(pf_ctx *ctx, const pf_problem *pb, const pf_fit_opts *opts, 
                    (!cv || (cv->n_groups == 1 && cv->window == cv->n_rows)) && !getenv_flag("PF_NO_FUSE");
   const bool only = (flags & PF_FF_ONLY_FUSED) != 0;
   if (!can && only) return 0;
+  const hipStream_t st0 = (hipStream_t)stream;
+  if (can) {
+    // K5 work-sharing counters (FuseArgs.ctl), zeroed on the stream
+    const int n = pb->n_series;
+    void *w = nullptr;
+    rc = ctx_workspace2(ctx, sizeof(int) * (size_t)(2 + 3 * n), &w);
+    if (rc) return rc;
+    fa.ctl = (int *)w;
+    PF_HIP(ctx, hipMemsetAsync(fa.ctl, 0, sizeof(int) * (size_t)(2 + 3 * n), st0));
+    PF_HIP(ctx, hipMemsetD32Async((hipDeviceptr_t)(fa.ctl + 1), n * PF_FF_BLOCKS, 1, st0));
+  }
   FuseReq fz{&fa, only ? 1 : 0, 0};
   FitKArgs a = make_fit_args(pb);
   a.theta = theta_inout;

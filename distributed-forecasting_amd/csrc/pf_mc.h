@@ -529,16 +529,19 @@ __device__ __forceinline__ void mc_rows(const PredKArgs &a, const PredSeries &ps
   }
 }
 
+template <bool TR>
+__device__ __forceinline__ void mc_block_rows(const PredKArgs &a, const PredSeries &ps, int series, uint32_t sid,
+                                              int bx, int gdx, const float2 *s_cp, const uint32_t *s_meta,
+                                              float *s_buf, const double *s_wsum, const int *s_r0);
+
 // One block's share of a series' Monte-Carlo rows (block bx of gdx over the
 // random rows), the series' PredSeries already set up in ps (pred_setup +
 // a block barrier).  LDS: s_cp [PF_MC_CPCAP], s_meta [64 PF_NQ], s_buf
 // [PF_MC_WAVES][4 * 64], s_wsum [PF_MC_WAVES], s_r0 [1].  A wave without rows
 // returns early (no block-level sync after the setup).  Shared by
 // k_predict_mc and the fused forecast epilogue (k_fit_forecast).
-template <bool TR>
-__device__ __forceinline__ void mc_block(const PredKArgs &a, const PredSeries &ps, int series, uint32_t sid,
-                                         int bx, int gdx, float2 *s_cp, uint32_t *s_meta, float *s_buf,
-                                         double *s_wsum, int *s_r0) {
+__device__ __forceinline__ void mc_setup(const PredKArgs &a, const PredSeries &ps, uint32_t sid,
+                                         float2 *s_cp, uint32_t *s_meta, double *s_wsum, int *s_r0) {
   constexpr int NT = PF_MC_WAVES * 64;
   constexpr int SPT = (64 * PF_NQ) / NT;  // samples per thread in the setup
   const int lane = pf_lane(), wave = pf_wave(), tid = threadIdx.x;
@@ -602,6 +605,28 @@ __device__ __forceinline__ void mc_block(const PredKArgs &a, const PredSeries &p
   }
   __syncthreads();
   PF_STAMP1(1);
+}
+
+template <bool TR>
+__device__ __forceinline__ void mc_block(const PredKArgs &a, const PredSeries &ps, int series, uint32_t sid,
+                                         int bx, int gdx, float2 *s_cp, uint32_t *s_meta, float *s_buf,
+                                         double *s_wsum, int *s_r0) {
+  mc_setup(a, ps, sid, s_cp, s_meta, s_wsum, s_r0);
+  mc_block_rows<TR>(a, ps, series, sid, bx, gdx, s_cp, s_meta, s_buf, s_wsum, s_r0);
+}
+
+// The row part of mc_block (after its setup: s_r0, s_cp / s_meta packed,
+// s_wsum's total): block bx of gdx over the random rows.  A workgroup that
+// ran the setup once can walk several of its series' blocks.
+template <bool TR>
+__device__ __forceinline__ void mc_block_rows(const PredKArgs &a, const PredSeries &ps, int series, uint32_t sid,
+                                              int bx, int gdx, const float2 *s_cp, const uint32_t *s_meta,
+                                              float *s_buf, const double *s_wsum, const int *s_r0) {
+  const int wave = pf_wave();
+  const double t_max = a.t[a.Tf - 1];
+  double total = 0.0;
+  for (int w = 0; w < PF_MC_WAVES; ++w) total += s_wsum[w];
+  const bool ovf = total > (double)PF_MC_CPCAP;  // uniform
   const int r0 = *s_r0;
   const int nrows = a.Tf - r0;
   if (nrows <= 0) return;

@@ -53,6 +53,9 @@ def run(name, fn):
 
 
 run("forecast_store_items", lambda: dfa.forecast_store_items(df))
+os.environ["PF_NO_FUSE"] = "1"      # A/B: pf_fit_forecast runs the separate launches
+run("forecast_store_items (fuse off)", lambda: dfa.forecast_store_items(df))
+del os.environ["PF_NO_FUSE"]
 with tempfile.TemporaryDirectory() as tmp:
     store = dfa.ParamsStore(os.path.join(tmp, "params"), writer="r0")
     dfa.forecast_store_items(df, params_store=store)
