@@ -2349,8 +2349,12 @@ __device__ __forceinline__ void ff_setup(const FuseArgs &e, const PredSeries &ps
 // Row block b of series t (after ff_setup of t), then — for the workgroup
 // that finishes the series' last block — its K6 row.  Returns true when K6
 // ran (its APE cache overwrote the packed changepoints).  Every thread calls it.
-__device__ __forceinline__ bool ff_rows(const FuseArgs &e, const PredSeries &ps, int t, int b,
-                                        char *smem_raw, int *s_bcast) {
+#ifdef PF_FF_ROWS_NOINLINE
+__device__ __noinline__
+#else
+__device__ __forceinline__
+#endif
+bool ff_rows(const FuseArgs &e, const PredSeries &ps, int t, int b, char *smem_raw, int *s_bcast) {
   const PredKArgs &pa = e.p;
   const int n = pa.n_series;
   int *finished = e.ctl + 2 + 2 * n;
