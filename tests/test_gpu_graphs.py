@@ -225,3 +225,27 @@ def test_fit_forecast_falls_back_and_reports():
     torch.cuda.synchronize()
     assert not fused3 and met3 is not None
     assert torch.equal(_cols_bits(out3["yhat"], T), _cols_bits(o2["yhat"], T))
+
+
+def test_fused_step_more_series_than_resident_workgroups():
+    """1100 series (more workgroups than the GPU holds at once: the K5 work
+    sharing's helpers must not wait while workgroups are still to start) —
+    the fused launch still gives the separate launches' bits."""
+    ds = synthetic.daily_dates("2016-01-01", "2017-12-30")
+    n = 1100
+    Y = synthetic.sales_matrix(n, ds, config_index=3)
+    eng = dfa.Engine(0)
+    snaps = {}
+    for fuse in (True, False):
+        st = dfa.ForecastStep(eng, ds, n, metrics="fast", fuse=fuse)
+        st.set_inputs(Y)
+        r = st.run()
+        torch.cuda.synchronize()
+        assert st.fused is fuse
+        Tf = st.Tf
+        snaps[fuse] = {k: _cols_bits(v, Tf).clone() for k, v in r["forecast"].items()}
+        snaps[fuse]["metrics"] = _cols_bits(r["metrics"], 10 ** 6).clone()
+        snaps[fuse]["theta"] = _cols_bits(r["fit"].theta, 10 ** 6).clone()
+        st.close()
+    for k in snaps[True]:
+        assert torch.equal(snaps[True][k], snaps[False][k]), k
